@@ -1,0 +1,129 @@
+/*
+ * gpscore.h — C-ABI of libgpscore.so, the MI355X (gfx950) GP-regression hot path.
+ *
+ * Reference being replaced (polarlightman/Scoring-rules-for-Gaussian-process-
+ * regression..., aliases as in SURVEY.md §0: KF = kin40k-FULL-compare.py,
+ * K20 = KIN40K-COMPARE-ALL-FITC-20.py, SD = "SIMPLE-DATA FULL-comapre.py").
+ * The reference has no FFI; its call surface is module-level torch-CPU helpers.
+ * Each entry point below names the reference code it replaces.  The ctypes
+ * binding that a maintainer would add is gpscore/_lib.py.
+ *
+ * Conventions
+ *  - All arrays are caller-owned, C-contiguous, row-major float64 HOST arrays
+ *    unless the name ends in _dev; the library copies H2D/D2H itself.
+ *  - Device buffers are owned by the opaque context and reused across calls.
+ *  - Return value: 0 ok; >0 LAPACK-style info (the leading minor of that order
+ *    is not positive definite, as torch.potrf raises); <0 argument / HIP / RCCL
+ *    error, message via gps_last_error().  NaN/Inf propagate, nothing clamps.
+ *  - A context is bound to one device and one HIP stream; it is not thread-safe.
+ *  - theta layout everywhere: [log_sf2, log_ell_0 .. log_ell_{n_ell-1}, log_sn2]
+ *    (n_ell = 1 or d), the reference's log-parameterisation para_k, para_l,
+ *    para_noise (KF:7-12, KF:239).  kind: GPS_ARD (b = log ℓ) or GPS_RBF
+ *    (b = log ℓ², SD:8-21).
+ */
+#ifndef GPSCORE_H
+#define GPSCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gps_ctx gps_ctx;
+
+enum { GPS_ARD = 0, GPS_RBF = 1 };
+enum { GPS_FULL = 0, GPS_LOWER = 1 };
+
+/* objective vector written by the fit calls */
+enum {
+  GPS_OBJ_NLML = 0,      /* ½n·log2π + ½log|A| + ½yᵀA⁻¹y            KF:334 / K20:339-340 */
+  GPS_OBJ_LOO_CRPS = 1,  /* mean LOO CRPS                             KF:241-245 / K20:222-234 */
+  GPS_OBJ_LOO_LOGS = 2,  /* mean LOO log score                        KF:416-424 / K20:434-447 */
+  GPS_OBJ_LOGDET = 3,    /* log|A|                                    KF:332 (×2) */
+  GPS_OBJ_QUAD = 4,      /* yᵀA⁻¹y                                    KF:334 */
+  GPS_N_OBJ = 5
+};
+/* score vector written by gps_*_predict_score / gps_scores (KF:276-292) */
+enum {
+  GPS_SC_CRPS = 0, GPS_SC_LOGS = 1, GPS_SC_MSLL = 2, GPS_SC_SMSE = 3,
+  GPS_SC_MSE = 4, GPS_SC_COVER = 5, GPS_N_SC = 6
+};
+
+/* ---- context ------------------------------------------------------------ */
+int gps_version(void);
+int gps_ctx_create(int device, gps_ctx** out);
+int gps_ctx_destroy(gps_ctx* ctx);
+const char* gps_last_error(gps_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream) instead of the ctx's own. */
+int gps_ctx_set_stream(gps_ctx* ctx, void* hip_stream);
+void* gps_ctx_stream(gps_ctx* ctx);
+int gps_ctx_synchronize(gps_ctx* ctx);
+
+/* ---- per-kernel timing (hipEvents on the ctx stream) ---------------------- */
+int gps_prof_enable(gps_ctx* ctx, int on);
+/* Synchronises, then writes a JSON object {tag: {count, ms, flop, bytes}} and clears. */
+int gps_prof_collect(gps_ctx* ctx, char* json_out, int64_t cap);
+
+/* ---- L1 building blocks ---------------------------------------------------- */
+/* ARD(x, xp, a, b) KF:7-23 / rbf SD:8-21: out[n][m] = sf2·exp(−½‖(x−x')/ℓ‖²)
+ * (+ diag_add where i == j); uplo GPS_LOWER writes only j <= i. */
+int gps_gram(gps_ctx* ctx, int kind, const double* X, int64_t n, const double* Xp,
+             int64_t m, int d, double log_sf2, const double* log_ell, int n_ell,
+             double diag_add, int uplo, double* out);
+/* torch.potrf(A).diag().log().sum() (KF:332): lower Cholesky L written into A
+ * (lower triangle, upper zeroed); *logdet = log|A|.  Returns info > 0 if not PD. */
+int gps_potrf(gps_ctx* ctx, int64_t n, double* A, int64_t lda, double* logdet);
+/* chol_solve(B, A) KF:25-29: X = A⁻¹·B for SPD A (n×n) and B (n×nrhs). */
+int gps_potrs(gps_ctx* ctx, int64_t n, int64_t nrhs, const double* A, int64_t lda,
+              const double* B, int64_t ldb, double* X, int64_t ldx);
+/* diag(chol_solve(I, A)) KF:242: dinv[i] = (A⁻¹)_ii. */
+int gps_diag_inv(gps_ctx* ctx, int64_t n, const double* A, int64_t lda, double* dinv);
+/* torch.mm in the reference helpers (Q KF:38, cal_mean_and_cov KF:123-125,
+ * spgp_cal_mean_and_cov K20:81-82): C = alpha·op(A)·op(B) + beta·C on the FP64
+ * MFMA path; op(X) = Xᵀ when trans != 0. */
+int gps_gemm(gps_ctx* ctx, int transA, int transB, int64_t M, int64_t N, int64_t K, double alpha,
+             const double* A, int64_t lda, const double* B, int64_t ldb, double beta, double* C,
+             int64_t ldc);
+/* crps/logs/trivial_loss/SMSE/MSE/coverage of a Gaussian predictive (KF:52-68,
+ * 110-134, 276-292); var is the VARIANCE.  ytr_mean / ytr_var_unbiased are
+ * the train-target statistics trivial_loss and SMSE use. */
+int gps_scores(gps_ctx* ctx, const double* mu, const double* var, const double* y,
+               int64_t nt, double ytr_mean, double ytr_var_unbiased, double out[GPS_N_SC]);
+
+/* ---- full GP (fused hot path) --------------------------------------------- */
+/* Upload training data (kept resident until replaced). */
+int gps_full_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n, int d);
+int gps_full_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t nt);
+/* One forward evaluation of the per-iteration bodies KF:239-245, 329-334,
+ * 416-424 at theta: Gram + potrf + L⁻¹ + α + diag(A⁻¹) → objectives.
+ * mu_loo / var_loo (length n) may be NULL (kept on device). */
+int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell,
+                 double obj[GPS_N_OBJ], double* mu_loo, double* var_loo);
+/* Predictive mean/variance at the test points with the last fit's factor
+ * (cal_mean_and_cov KF:121-126, diag of the covariance), plus the score bundle
+ * against yt (KF:276-292).  mu / var may be NULL; sc may be NULL. */
+int gps_full_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]);
+
+/* ---- FITC sparse GP (Woodbury restatement of K20:32-39, 76-83, 222-340) ----- */
+int gps_fitc_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n, int d,
+                      double ytr_mean, double ytr_var_unbiased, int64_t n_total);
+int gps_fitc_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t nt,
+                      int64_t nt_total);
+int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m);
+/* FITC objectives over this rank's rows.  With a communicator (gps_comm_init)
+ * the m×m accumulator and scalar partials are all-reduced over RCCL; objectives
+ * are then global and mu_loo / var_loo hold this rank's rows. */
+int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
+                 double* mu_loo, double* var_loo);
+int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]);
+
+/* ---- multi-GPU (RCCL over xGMI) ------------------------------------------- */
+int gps_comm_unique_id(char uid[128]);
+int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]);
+int gps_comm_destroy(gps_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPSCORE_H */

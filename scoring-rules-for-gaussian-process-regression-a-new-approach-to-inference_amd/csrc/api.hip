@@ -1,0 +1,1040 @@
+// C-ABI of libgpscore.so (declared in include/gpscore.h): context, device
+// buffers, the recursive Cholesky + triangular-inverse driver, and the fused
+// full-GP / FITC pipelines.  Host orchestration only; the arithmetic lives in
+// kernels_*.hip.
+//
+// Full GP, one fit (KF:239-245 LOO-CRPS, KF:329-334 NLML, KF:416-424 LOO-LogS):
+//   A = K(X,X) + σ²I (lower)  →  [L, L⁻¹] = potrf_inv(A)  →  β = L⁻¹y
+//   → α = L⁻ᵀβ, d = diag(A⁻¹) = colsum(L⁻¹∘L⁻¹)  →  μ_loo = y − α/d, σ²_loo = 1/d
+//   NLML = ½n log2π + Σ log L_ii + ½‖β‖²
+// Full GP, predict (cal_mean_and_cov KF:121-126, diag only):
+//   V = L⁻¹ K_f*  (never stored: fused column reductions)  μ* = Vᵀβ,
+//   σ²* = σ² + sf2 − colsum(V∘V)
+// FITC (K20:222-340 restated, O(n m²)):
+//   λ = sf2 − ‖Lm⁻¹k_i‖² + σ², B = K̃mm + KmnΛ⁻¹Knm (split-K SYRK, RCCL all-reduce
+//   across row shards), c = B⁻¹KmnΛ⁻¹y, diag((Q+Λ)⁻¹) = 1/λ − ‖Lb⁻¹k_i‖²/λ²,
+//   log|Q+Λ| = Σlogλ + log|B| − log|K̃mm|.
+//
+// potrf_inv (recursive, all O(n³) work in the MFMA GEMM):
+//   [L11, L11⁻¹] = rec(A11);  L21 = A21 L11⁻ᵀ;  A22 −= L21 L21ᵀ;
+//   T = L21 L11⁻¹ (into A21);  [L22, L22⁻¹] = rec(A22);  L⁻¹21 = −L22⁻¹ T
+//   → n³/3 (potrf) + n³/3 (trtri) flops; base case: 128×128 LDS kernel.
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <climits>
+#include <cmath>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "gps_internal.h"
+#include "gpscore.h"
+
+using namespace gps;
+
+namespace {
+
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  double* d() const { return static_cast<double*>(p); }
+};
+
+struct ProfRec {
+  std::string tag;
+  int e0, e1;
+  double flop, bytes;
+};
+
+struct Theta {
+  int kind = GPS_ARD;
+  double sf2 = 1.0, sn2 = 1.0;
+  double inv_ell[GPS_MAX_D];
+};
+
+}  // namespace
+
+struct gps_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  std::string err;
+  // profiling
+  bool prof = false;
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  std::vector<ProfRec> recs;
+  // pinned host staging for small results
+  double* hsmall = nullptr;
+  int* hinfo = nullptr;
+  // generic scratch
+  DBuf info, small;
+  // ---- full GP state
+  DBuf X, y, Xt, yt, A, Linv, W, logdiag, beta, alpha, dinv, slab, mu_loo, var_loo, Ksf, s1, s2,
+      mu, var, Lout;
+  size_t linv_zeroed = 0;
+  int64_t n = 0, n_pad = 0, nt = 0, nt_pad = 0;
+  int d = 0;
+  double ytr_mean = 0, ytr_var = 1;
+  bool have_data = false, have_test = false, fitted = false;
+  Theta th;
+  // ---- FITC state
+  DBuf fX, fy, fXt, fyt, Z, Kmm, Am, Lm, Lb, ldm, ldb, Knm, q, lam, ilam, ys, slabB, red, c, tvec,
+      r, g, fmu_loo, fvar_loo, Ksm, qm, qb, fmu, fvar, fslab;
+  size_t lm_zeroed = 0, lb_zeroed = 0;
+  int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
+  int fd = 0;
+  double f_ytr_mean = 0, f_ytr_var = 1;
+  bool f_data = false, f_test = false, f_z = false, f_fitted = false;
+  Theta fth;
+  // ---- comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // ---- compat scratch (gps_gram / potrf / potrs / diag_inv / scores)
+  DBuf t0, t1, t2, t3, t4;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(gps_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      return fail(ctx, -2, std::string(#expr) + " failed: " + hipGetErrorString(_e));   \
+  } while (0)
+
+#define NCCLCHK(expr)                                                                     \
+  do {                                                                                    \
+    ncclResult_t _r = (expr);                                                             \
+    if (_r != ncclSuccess)                                                                \
+      return fail(ctx, -3, std::string(#expr) + " failed: " + ncclGetErrorString(_r));  \
+  } while (0)
+
+#define ARGCHK(cond, msg)                  \
+  do {                                     \
+    if (!(cond)) return fail(ctx, -1, msg); \
+  } while (0)
+
+hipError_t ensure(DBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return hipSuccess;
+  if (b.p) {
+    hipError_t e = hipFree(b.p);
+    if (e != hipSuccess) return e;
+  }
+  b.p = nullptr;
+  b.cap = 0;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e == hipSuccess) b.cap = bytes;
+  return e;
+}
+void release(DBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+// ------------------------------------------------------------------ profiling
+int get_event(gps_ctx* c) {
+  if (c->ev_used == c->ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    c->ev.push_back(e);
+  }
+  return (int)c->ev_used++;
+}
+
+struct Prof {
+  gps_ctx* c;
+  int e0 = -1;
+  const char* tag;
+  double flop, bytes;
+  Prof(gps_ctx* c_, const char* t, double f, double b) : c(c_), tag(t), flop(f), bytes(b) {
+    if (c->prof && (e0 = get_event(c)) >= 0) (void)hipEventRecord(c->ev[e0], c->stream);
+  }
+  ~Prof() {
+    if (!c->prof || e0 < 0) return;
+    const int e1 = get_event(c);
+    if (e1 < 0) return;
+    (void)hipEventRecord(c->ev[e1], c->stream);
+    c->recs.push_back({tag, e0, e1, flop, bytes});
+  }
+};
+
+// --------------------------------------------------------------- launch helpers
+GemmParams gp0() {
+  GemmParams p;
+  memset(&p, 0, sizeof(p));
+  p.alpha = 1.0;
+  p.ksplit = 1;
+  return p;
+}
+
+const char* gemm_tag(int al, int bl, int epi, const GemmParams& p) {
+  if (epi == EPI_COLRED) return "gemm_trmm_colred";
+  if (epi == EPI_ROWSQ) return "gemm_rowsq";
+  if (p.lower_out) return p.ksplit > 1 ? "gemm_syrk_splitk" : "gemm_syrk";
+  (void)al;
+  (void)bl;
+  return p.tri ? "gemm_trmm" : "gemm";
+}
+
+// algorithmic flops of one launch (triangular operands counted at their nonzero half)
+double gemm_flops(const GemmParams& p) {
+  const double M = p.M, N = p.N, K = p.K;
+  if (p.lower_out) return M * (M + 1) * K;  // SYRK, lower half
+  if (p.tri) return M * N * K;              // triangular operand: half of 2MNK
+  return 2.0 * M * N * K;
+}
+
+int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p) {
+  Prof pr(ctx, gemm_tag(al, bl, epi, p), gemm_flops(p), 0);
+  HIPCHK(launch_gemm(al, bl, epi, p, ctx->stream));
+  return 0;
+}
+
+int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp, int m, int d,
+         const Theta& th, double diag_add, int lower, int pad_identity, double* out, int64_t ldo,
+         int M, int N) {
+  GramParams g;
+  memset(&g, 0, sizeof(g));
+  g.x = x;
+  g.xp = xp;
+  g.out = out;
+  g.ldo = ldo;
+  g.n = n;
+  g.m = m;
+  g.M = M;
+  g.N = N;
+  g.d = d;
+  g.sf2 = th.sf2;
+  g.diag_add = diag_add;
+  g.lower = lower;
+  g.pad_identity = pad_identity;
+  for (int k = 0; k < d; ++k) g.inv_ell[k] = th.inv_ell[k];
+  const double elems = lower ? 0.5 * (double)M * (M + 1) : (double)M * N;
+  Prof pr(ctx, tag, 0, 8.0 * elems);
+  HIPCHK(launch_gram(g, ctx->stream));
+  return 0;
+}
+
+// recursive Cholesky + inverse on a padded (multiple of 128) SPD block
+int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
+                  int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
+                  int64_t ldlo) {
+  hipStream_t s = ctx->stream;
+  if (nb == 1) {
+    Prof pr(ctx, "potrf_diag128", 2.0 * 128 * 128 * 128 / 3.0, 0);
+    HIPCHK(launch_potrf_diag(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, s));
+    return 0;
+  }
+  const int n1b = nb / 2, n2b = nb - n1b;
+  const int n1 = n1b * GPS_TILE, n2 = n2b * GPS_TILE;
+  double* A21 = A + (int64_t)n1 * lda;
+  double* A22 = A21 + n1;
+  double* Li21 = Linv + (int64_t)n1 * ldl;
+  double* Li22 = Li21 + n1;
+  int rc;
+  if ((rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo)))
+    return rc;
+  {  // W = L21 = A21 · L11⁻ᵀ
+    GemmParams p = gp0();
+    p.A = A21; p.lda = lda; p.B = Linv; p.ldb = ldl; p.C = W; p.ldc = n1;
+    p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_LE_J;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
+  }
+  if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
+                                    (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
+  {  // A22 -= L21 L21ᵀ  (lower tiles)
+    GemmParams p = gp0();
+    p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
+    p.M = n2; p.N = n2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
+  }
+  {  // T = L21 · L11⁻¹  → A21
+    GemmParams p = gp0();
+    p.A = W; p.lda = n1; p.B = Linv; p.ldb = ldl; p.C = A21; p.ldc = lda;
+    p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
+  }
+  if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W, n2b, logdiag + n1, info, base + n1,
+                          nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr, ldlo)))
+    return rc;
+  {  // L⁻¹21 = −L22⁻¹ · T
+    GemmParams p = gp0();
+    p.A = Li22; p.lda = ldl; p.B = A21; p.ldb = lda; p.C = Li21; p.ldc = ldl;
+    p.M = n2; p.N = n1; p.K = n2; p.alpha = -1.0; p.tri = TRI_K_LE_I;
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
+  }
+  return 0;
+}
+
+size_t potrf_ws_doubles(int64_t n_pad) {
+  const int64_t nb = n_pad / GPS_TILE;
+  const int64_t n1 = (nb / 2) * GPS_TILE, n2 = n_pad - n1;
+  return (size_t)std::max<int64_t>(n1 * n2, GPS_TILE * GPS_TILE);
+}
+
+// factor the padded SPD matrix in A (destroyed) into Linv (must be zero in strict-upper
+// tiles), logdiag (n_pad).  Returns 0 or the LAPACK-style info (> 0).
+int reset_info(gps_ctx* ctx) {
+  HIPCHK(hipMemsetAsync(ctx->info.p, 0x7f, sizeof(int), ctx->stream));
+  return 0;
+}
+
+int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
+              int nreal, double* Lout) {
+  int rc = potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
+                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad);
+  return rc;
+}
+
+int check_info(gps_ctx* ctx) {
+  HIPCHK(hipMemcpyAsync(ctx->hinfo, ctx->info.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const int info = *ctx->hinfo;
+  if (info != 0x7f7f7f7f) {
+    char buf[160];
+    snprintf(buf, sizeof(buf),
+             "cholesky: the leading minor of order %d is not positive definite", info);
+    return fail(ctx, info, buf);
+  }
+  return 0;
+}
+
+int set_theta(gps_ctx* ctx, Theta& th, int kind, const double* theta, int n_ell, int d) {
+  ARGCHK(theta != nullptr, "theta is NULL");
+  ARGCHK(kind == GPS_ARD || kind == GPS_RBF, "kind must be GPS_ARD or GPS_RBF");
+  ARGCHK(n_ell == 1 || n_ell == d, "n_ell must be 1 or d");
+  th.kind = kind;
+  th.sf2 = std::exp(theta[0]);
+  th.sn2 = std::exp(theta[1 + n_ell]);
+  for (int k = 0; k < d; ++k) {
+    const double b = theta[1 + (n_ell == 1 ? 0 : k)];
+    th.inv_ell[k] = kind == GPS_ARD ? std::exp(-b) : std::exp(-0.5 * b);
+  }
+  return 0;
+}
+
+int upload(gps_ctx* ctx, DBuf& b, const double* h, int64_t rows, int64_t cols, int64_t rows_pad) {
+  HIPCHK(ensure(b, (size_t)rows_pad * cols * 8));
+  HIPCHK(hipMemsetAsync(b.p, 0, (size_t)rows_pad * cols * 8, ctx->stream));
+  if (rows * cols)
+    HIPCHK(hipMemcpyAsync(b.p, h, (size_t)rows * cols * 8, hipMemcpyHostToDevice, ctx->stream));
+  return 0;
+}
+
+void score_bundle(const double* sums, double nt, double out[GPS_N_SC]) {
+  out[GPS_SC_CRPS] = sums[0] / nt;
+  out[GPS_SC_LOGS] = sums[1] / nt;
+  out[GPS_SC_MSLL] = sums[2] / nt;
+  out[GPS_SC_SMSE] = sums[3] / sums[4];
+  out[GPS_SC_MSE] = sums[3] / nt;
+  out[GPS_SC_COVER] = sums[5] / nt;
+}
+
+int bind(gps_ctx* ctx) {
+  if (!ctx) {
+    g_err = "NULL context";
+    return -1;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  return 0;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+int gps_version(void) { return 100; }
+
+int gps_ctx_create(int device, gps_ctx** out) {
+  gps_ctx* ctx = nullptr;
+  if (!out) return fail(nullptr, -1, "out is NULL");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return fail(nullptr, -2, std::string("no HIP device: ") + hipGetErrorString(e));
+  if (device < 0 || device >= ndev) return fail(nullptr, -1, "device index out of range");
+  ctx = new gps_ctx();
+  ctx->device = device;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  HIPCHK(hipHostMalloc((void**)&ctx->hsmall, 256 * sizeof(double), hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)&ctx->hinfo, 16, hipHostMallocDefault));
+  HIPCHK(ensure(ctx->info, 16));
+  HIPCHK(ensure(ctx->small, 256 * sizeof(double)));
+  *out = ctx;
+  return 0;
+}
+
+int gps_ctx_destroy(gps_ctx* ctx) {
+  if (!ctx) return 0;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  DBuf* all[] = {&ctx->info, &ctx->small, &ctx->X, &ctx->y, &ctx->Xt, &ctx->yt, &ctx->A,
+                 &ctx->Linv, &ctx->W, &ctx->logdiag, &ctx->beta, &ctx->alpha, &ctx->dinv,
+                 &ctx->slab, &ctx->mu_loo, &ctx->var_loo, &ctx->Ksf, &ctx->s1, &ctx->s2,
+                 &ctx->mu, &ctx->var, &ctx->Lout, &ctx->fX, &ctx->fy, &ctx->fXt, &ctx->fyt,
+                 &ctx->Z, &ctx->Kmm, &ctx->Am, &ctx->Lm, &ctx->Lb, &ctx->ldm, &ctx->ldb,
+                 &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
+                 &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
+                 &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
+                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4};
+  for (DBuf* b : all) release(*b);
+  for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
+  if (ctx->hsmall) (void)hipHostFree(ctx->hsmall);
+  if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
+  if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return 0;
+}
+
+const char* gps_last_error(gps_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int gps_ctx_set_stream(gps_ctx* ctx, void* hip_stream) {
+  if (int rc = bind(ctx)) return rc;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->own_stream && ctx->stream) HIPCHK(hipStreamDestroy(ctx->stream));
+  if (hip_stream) {
+    ctx->stream = static_cast<hipStream_t>(hip_stream);
+    ctx->own_stream = false;
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    ctx->own_stream = true;
+  }
+  return 0;
+}
+
+void* gps_ctx_stream(gps_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int gps_ctx_synchronize(gps_ctx* ctx) {
+  if (int rc = bind(ctx)) return rc;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_prof_enable(gps_ctx* ctx, int on) {
+  if (int rc = bind(ctx)) return rc;
+  ctx->prof = on != 0;
+  return 0;
+}
+
+int gps_prof_collect(gps_ctx* ctx, char* json_out, int64_t cap) {
+  if (int rc = bind(ctx)) return rc;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  struct Agg { int count = 0; double ms = 0, flop = 0, bytes = 0; };
+  std::map<std::string, Agg> agg;
+  for (const ProfRec& r : ctx->recs) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev[r.e0], ctx->ev[r.e1]));
+    Agg& a = agg[r.tag];
+    a.count++;
+    a.ms += ms;
+    a.flop += r.flop;
+    a.bytes += r.bytes;
+  }
+  ctx->recs.clear();
+  ctx->ev_used = 0;
+  std::string js = "{";
+  bool first = true;
+  for (auto& kv : agg) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s\"%s\": {\"count\": %d, \"ms\": %.6f, \"flop\": %.6e, \"bytes\": %.6e}",
+             first ? "" : ", ", kv.first.c_str(), kv.second.count, kv.second.ms, kv.second.flop,
+             kv.second.bytes);
+    js += buf;
+    first = false;
+  }
+  js += "}";
+  if (!json_out || cap <= (int64_t)js.size()) return fail(ctx, -1, "json buffer too small");
+  memcpy(json_out, js.c_str(), js.size() + 1);
+  return 0;
+}
+
+// ------------------------------------------------------------------ L1 blocks
+int gps_gram(gps_ctx* ctx, int kind, const double* X, int64_t n, const double* Xp, int64_t m, int d,
+             double log_sf2, const double* log_ell, int n_ell, double diag_add, int uplo,
+             double* out) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(X && Xp && out && log_ell, "NULL argument");
+  ARGCHK(n > 0 && m > 0 && d >= 1 && d <= GPS_MAX_D, "bad shape");
+  ARGCHK(uplo == GPS_FULL || (uplo == GPS_LOWER && n == m), "uplo=LOWER needs a square Gram");
+  std::vector<double> theta(n_ell + 2);
+  theta[0] = log_sf2;
+  for (int k = 0; k < n_ell; ++k) theta[1 + k] = log_ell[k];
+  theta[1 + n_ell] = 0.0;
+  Theta th;
+  if (int rc = set_theta(ctx, th, kind, theta.data(), n_ell, d)) return rc;
+  const int64_t M = pad_to(n, 32), N = pad_to(m);
+  if (int rc = upload(ctx, ctx->t0, X, n, d, n)) return rc;
+  if (int rc = upload(ctx, ctx->t1, Xp, m, d, m)) return rc;
+  HIPCHK(ensure(ctx->t2, (size_t)M * N * 8));
+  HIPCHK(hipMemsetAsync(ctx->t2.p, 0, (size_t)M * N * 8, ctx->stream));
+  if (int rc = gram(ctx, "gram_user", ctx->t0.d(), (int)n, ctx->t1.d(), (int)m, d, th, diag_add,
+                    uplo == GPS_LOWER, 0, ctx->t2.d(), N, (int)M, (int)N))
+    return rc;
+  HIPCHK(hipMemcpy2DAsync(out, (size_t)m * 8, ctx->t2.p, (size_t)N * 8, (size_t)m * 8, n,
+                          hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// helper: bring a user SPD matrix to the device padded with identity, factor it
+static int factor_user(gps_ctx* ctx, int64_t n, const double* A, int64_t lda, bool want_L) {
+  ARGCHK(A && n > 0 && lda >= n, "bad matrix argument");
+  const int64_t np = pad_to(n);
+  HIPCHK(ensure(ctx->t0, (size_t)n * lda * 8));
+  HIPCHK(hipMemcpyAsync(ctx->t0.p, A, (size_t)n * lda * 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ensure(ctx->t1, (size_t)np * np * 8));
+  HIPCHK(launch_pad_copy(ctx->t0.d(), lda, ctx->t1.d(), np, (int)n, (int)n, (int)np, (int)np, 1,
+                         ctx->stream));
+  HIPCHK(ensure(ctx->t2, (size_t)np * np * 8));
+  HIPCHK(hipMemsetAsync(ctx->t2.p, 0, (size_t)np * np * 8, ctx->stream));  // L⁻¹ upper tiles = 0
+  HIPCHK(ensure(ctx->t3, potrf_ws_doubles(np) * 8));
+  HIPCHK(ensure(ctx->t4, (size_t)np * 8 * (want_L ? np + 1 : 1)));
+  double* logdiag = ctx->t4.d();
+  double* Lout = want_L ? ctx->t4.d() + np : nullptr;
+  if (want_L) HIPCHK(hipMemsetAsync(Lout, 0, (size_t)np * np * 8, ctx->stream));
+  if (int rc = reset_info(ctx)) return rc;
+  if (int rc = potrf_inv(ctx, ctx->t1.d(), np, ctx->t2.d(), ctx->t3.d(), logdiag, (int)n, Lout))
+    return rc;
+  return check_info(ctx);
+}
+
+int gps_potrf(gps_ctx* ctx, int64_t n, double* A, int64_t lda, double* logdet) {
+  if (int rc = bind(ctx)) return rc;
+  if (int rc = factor_user(ctx, n, A, lda, true)) return rc;
+  const int64_t np = pad_to(n);
+  HIPCHK(launch_dot(ctx->t4.d(), nullptr, (int)np, ctx->small.d(), ctx->stream));
+  HIPCHK(hipMemcpy2DAsync(A, (size_t)lda * 8, ctx->t4.d() + np, (size_t)np * 8, (size_t)n * 8, n,
+                          hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (logdet) *logdet = 2.0 * ctx->hsmall[0];
+  return 0;
+}
+
+int gps_potrs(gps_ctx* ctx, int64_t n, int64_t nrhs, const double* A, int64_t lda, const double* B,
+              int64_t ldb, double* X, int64_t ldx) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(B && X && nrhs > 0 && ldb >= nrhs && ldx >= nrhs, "bad rhs argument");
+  if (int rc = factor_user(ctx, n, A, lda, false)) return rc;
+  const int64_t np = pad_to(n), rp = pad_to(nrhs);
+  // B padded into t0 (reuse), Y = L⁻¹B into t1, X = L⁻ᵀY into t3
+  HIPCHK(ensure(ctx->t0, (size_t)n * ldb * 8));
+  HIPCHK(hipMemcpyAsync(ctx->t0.p, B, (size_t)n * ldb * 8, hipMemcpyHostToDevice, ctx->stream));
+  DBuf Bp, Y;
+  HIPCHK(ensure(Bp, (size_t)np * rp * 8));
+  HIPCHK(ensure(Y, (size_t)np * rp * 8));
+  int rc = 0;
+  do {
+    hipError_t e = launch_pad_copy(ctx->t0.d(), ldb, Bp.d(), rp, (int)n, (int)nrhs, (int)np,
+                                   (int)rp, 0, ctx->stream);
+    if (e != hipSuccess) { rc = fail(ctx, -2, hipGetErrorString(e)); break; }
+    GemmParams p = gp0();
+    p.A = ctx->t2.d(); p.lda = np; p.B = Bp.d(); p.ldb = rp; p.C = Y.d(); p.ldc = rp;
+    p.M = (int)np; p.N = (int)rp; p.K = (int)np; p.tri = TRI_K_LE_I;
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) break;
+    GemmParams q = gp0();
+    q.A = ctx->t2.d(); q.lda = np; q.B = Y.d(); q.ldb = rp; q.C = Bp.d(); q.ldc = rp;
+    q.M = (int)np; q.N = (int)rp; q.K = (int)np; q.tri = TRI_K_GE_I;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, q))) break;
+    e = hipMemcpy2DAsync(X, (size_t)ldx * 8, Bp.p, (size_t)rp * 8, (size_t)nrhs * 8, n,
+                         hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = fail(ctx, -2, hipGetErrorString(e));
+  } while (0);
+  release(Bp);
+  release(Y);
+  return rc;
+}
+
+int gps_diag_inv(gps_ctx* ctx, int64_t n, const double* A, int64_t lda, double* dinv) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(dinv, "dinv is NULL");
+  if (int rc = factor_user(ctx, n, A, lda, false)) return rc;
+  const int64_t np = pad_to(n);
+  const int64_t nchunk = (np + 255) / 256;
+  HIPCHK(ensure(ctx->t0, (size_t)(nchunk * np * 2 + np) * 8));
+  double* out = ctx->t0.d() + nchunk * np * 2;
+  HIPCHK(launch_colred(ctx->t2.d(), np, (int)np, (int)np, 1, nullptr, nullptr, nullptr, out,
+                       ctx->t0.d(), ctx->stream));
+  HIPCHK(hipMemcpyAsync(dinv, out, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_gemm(gps_ctx* ctx, int transA, int transB, int64_t M, int64_t N, int64_t K, double alpha,
+             const double* A, int64_t lda, const double* B, int64_t ldb, double beta, double* C,
+             int64_t ldc) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(A && B && C && M > 0 && N > 0 && K > 0, "bad gemm argument");
+  const int64_t Mp = pad_to(M), Np = pad_to(N), Kp = pad_to(K);
+  // stored shapes of A and B
+  const int64_t ar = transA ? K : M, ac = transA ? M : K, arp = transA ? Kp : Mp, acp = transA ? Mp : Kp;
+  const int64_t br = transB ? N : K, bc = transB ? K : N, brp = transB ? Np : Kp, bcp = transB ? Kp : Np;
+  ARGCHK(lda >= ac && ldb >= bc && ldc >= N, "leading dimension too small");
+  HIPCHK(ensure(ctx->t0, (size_t)(ar * lda + br * ldb + M * ldc) * 8));
+  double* rawA = ctx->t0.d();
+  double* rawB = rawA + ar * lda;
+  double* rawC = rawB + br * ldb;
+  HIPCHK(hipMemcpyAsync(rawA, A, (size_t)ar * lda * 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(rawB, B, (size_t)br * ldb * 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ensure(ctx->t1, (size_t)(arp * acp + brp * bcp + Mp * Np) * 8));
+  double* pA = ctx->t1.d();
+  double* pB = pA + arp * acp;
+  double* pC = pB + brp * bcp;
+  HIPCHK(launch_pad_copy(rawA, lda, pA, acp, (int)ar, (int)ac, (int)arp, (int)acp, 0, ctx->stream));
+  HIPCHK(launch_pad_copy(rawB, ldb, pB, bcp, (int)br, (int)bc, (int)brp, (int)bcp, 0, ctx->stream));
+  if (beta != 0.0) {
+    HIPCHK(hipMemcpyAsync(rawC, C, (size_t)M * ldc * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_pad_copy(rawC, ldc, pC, Np, (int)M, (int)N, (int)Mp, (int)Np, 0, ctx->stream));
+  }
+  GemmParams p = gp0();
+  p.A = pA; p.lda = acp; p.B = pB; p.ldb = bcp; p.C = pC; p.ldc = Np;
+  p.M = (int)Mp; p.N = (int)Np; p.K = (int)Kp; p.alpha = alpha; p.beta = beta;
+  if (int rc = gemm(ctx, transA ? LAY_T : LAY_N, transB ? LAY_T : LAY_N, EPI_STORE, p)) return rc;
+  HIPCHK(hipMemcpy2DAsync(C, (size_t)ldc * 8, pC, (size_t)Np * 8, (size_t)N * 8, M,
+                          hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_scores(gps_ctx* ctx, const double* mu, const double* var, const double* y, int64_t nt,
+               double ytr_mean, double ytr_var_unbiased, double out[GPS_N_SC]) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(mu && var && y && out && nt > 0, "bad argument");
+  if (int rc = upload(ctx, ctx->t0, mu, nt, 1, nt)) return rc;
+  if (int rc = upload(ctx, ctx->t1, var, nt, 1, nt)) return rc;
+  if (int rc = upload(ctx, ctx->t2, y, nt, 1, nt)) return rc;
+  HIPCHK(launch_score_sums(ctx->t0.d(), ctx->t1.d(), ctx->t2.d(), (int)nt, ytr_mean,
+                           ytr_var_unbiased, ctx->small.d(), ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, 6 * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  score_bundle(ctx->hsmall, (double)nt, out);
+  return 0;
+}
+
+// ------------------------------------------------------------------- full GP
+int gps_full_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n, int d) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(X && y && n > 1 && d >= 1 && d <= GPS_MAX_D, "bad training data");
+  ARGCHK(n <= (int64_t)1 << 30, "n too large");
+  ctx->n = n;
+  ctx->d = d;
+  ctx->n_pad = pad_to(n);
+  if (int rc = upload(ctx, ctx->X, X, n, d, ctx->n_pad)) return rc;
+  if (int rc = upload(ctx, ctx->y, y, n, 1, ctx->n_pad)) return rc;
+  double s = 0, s2 = 0;
+  for (int64_t i = 0; i < n; ++i) s += y[i];
+  const double mean = s / n;
+  for (int64_t i = 0; i < n; ++i) s2 += (y[i] - mean) * (y[i] - mean);
+  ctx->ytr_mean = mean;
+  ctx->ytr_var = s2 / (n - 1);
+  ctx->have_data = true;
+  ctx->fitted = false;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_full_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t nt) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->have_data, "gps_full_set_data first");
+  ARGCHK(Xt && nt > 0, "bad test data");
+  ctx->nt = nt;
+  ctx->nt_pad = pad_to(nt);
+  if (int rc = upload(ctx, ctx->Xt, Xt, nt, ctx->d, ctx->nt_pad)) return rc;
+  std::vector<double> zeros;
+  if (!yt) zeros.assign(nt, 0.0);
+  if (int rc = upload(ctx, ctx->yt, yt ? yt : zeros.data(), nt, 1, ctx->nt_pad)) return rc;
+  ctx->have_test = true;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell, double obj[GPS_N_OBJ],
+                 double* mu_loo, double* var_loo) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->have_data, "gps_full_set_data first");
+  if (int rc = set_theta(ctx, ctx->th, kind, theta, n_ell, ctx->d)) return rc;
+  const int64_t n = ctx->n, np = ctx->n_pad;
+  hipStream_t s = ctx->stream;
+  HIPCHK(ensure(ctx->A, (size_t)np * np * 8));
+  if (ctx->Linv.cap < (size_t)np * np * 8 || ctx->linv_zeroed != (size_t)np) {
+    HIPCHK(ensure(ctx->Linv, (size_t)np * np * 8));
+    HIPCHK(hipMemsetAsync(ctx->Linv.p, 0, (size_t)np * np * 8, s));
+    ctx->linv_zeroed = (size_t)np;
+  }
+  HIPCHK(ensure(ctx->W, potrf_ws_doubles(np) * 8));
+  HIPCHK(ensure(ctx->logdiag, np * 8));
+  HIPCHK(ensure(ctx->beta, np * 8));
+  HIPCHK(ensure(ctx->alpha, np * 8));
+  HIPCHK(ensure(ctx->dinv, np * 8));
+  HIPCHK(ensure(ctx->mu_loo, np * 8));
+  HIPCHK(ensure(ctx->var_loo, np * 8));
+  const int64_t nchunk = (np + 255) / 256;
+  HIPCHK(ensure(ctx->slab, (size_t)nchunk * np * 2 * 8));
+  int rc;
+  if ((rc = reset_info(ctx))) return rc;
+  if ((rc = gram(ctx, "gram_kff", ctx->X.d(), (int)n, ctx->X.d(), (int)n, ctx->d, ctx->th,
+                 ctx->th.sn2, 1, 1, ctx->A.d(), np, (int)np, (int)np)))
+    return rc;
+  if ((rc = potrf_inv(ctx, ctx->A.d(), np, ctx->Linv.d(), ctx->W.d(), ctx->logdiag.d(), (int)n,
+                      nullptr)))
+    return rc;
+  {
+    Prof pr(ctx, "gemv_beta", 0, 4.0 * (double)np * np);
+    HIPCHK(launch_gemv_lower(ctx->Linv.d(), np, ctx->y.d(), ctx->beta.d(), (int)np, s));
+  }
+  {
+    Prof pr(ctx, "colred_alpha_dinv", 0, 4.0 * (double)np * np);
+    HIPCHK(launch_colred(ctx->Linv.d(), np, (int)np, (int)np, 1, ctx->beta.d(), nullptr,
+                         ctx->alpha.d(), ctx->dinv.d(), ctx->slab.d(), s));
+  }
+  {
+    Prof pr(ctx, "loo_finalize", 0, 0);
+    HIPCHK(launch_full_loo(ctx->y.d(), ctx->alpha.d(), ctx->dinv.d(), ctx->beta.d(),
+                           ctx->logdiag.d(), (int)n, ctx->mu_loo.d(), ctx->var_loo.d(),
+                           ctx->small.d(), s));
+  }
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, GPS_N_OBJ * 8, hipMemcpyDeviceToHost, s));
+  if ((rc = check_info(ctx))) return rc;
+  if (obj)
+    for (int q = 0; q < GPS_N_OBJ; ++q) obj[q] = ctx->hsmall[q];
+  if (mu_loo) HIPCHK(hipMemcpyAsync(mu_loo, ctx->mu_loo.p, n * 8, hipMemcpyDeviceToHost, s));
+  if (var_loo) HIPCHK(hipMemcpyAsync(var_loo, ctx->var_loo.p, n * 8, hipMemcpyDeviceToHost, s));
+  if (mu_loo || var_loo) HIPCHK(hipStreamSynchronize(s));
+  ctx->fitted = true;
+  return 0;
+}
+
+int gps_full_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->fitted, "gps_full_fit first");
+  ARGCHK(ctx->have_test, "gps_full_set_test first");
+  const int64_t n = ctx->n, np = ctx->n_pad, nt = ctx->nt, ntp = ctx->nt_pad;
+  hipStream_t s = ctx->stream;
+  const int64_t tiles_m = np / GPS_TILE;
+  HIPCHK(ensure(ctx->Ksf, (size_t)ntp * np * 8));
+  HIPCHK(ensure(ctx->slab, std::max(ctx->slab.cap, (size_t)tiles_m * ntp * 2 * 8)));
+  HIPCHK(ensure(ctx->s1, ntp * 8));
+  HIPCHK(ensure(ctx->s2, ntp * 8));
+  HIPCHK(ensure(ctx->mu, ntp * 8));
+  HIPCHK(ensure(ctx->var, ntp * 8));
+  int rc;
+  if ((rc = gram(ctx, "gram_ksf", ctx->Xt.d(), (int)nt, ctx->X.d(), (int)n, ctx->d, ctx->th, 0.0, 0,
+                 0, ctx->Ksf.d(), np, (int)ntp, (int)np)))
+    return rc;
+  {
+    GemmParams p = gp0();
+    p.A = ctx->Linv.d(); p.lda = np; p.B = ctx->Ksf.d(); p.ldb = np;
+    p.M = (int)np; p.N = (int)ntp; p.K = (int)np; p.tri = TRI_K_LE_I;
+    p.w = ctx->beta.d(); p.out0 = ctx->slab.d(); p.out1 = ctx->slab.d() + tiles_m * ntp;
+    p.ld_out = ntp;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_COLRED, p))) return rc;
+  }
+  {
+    Prof pr(ctx, "pred_finalize", 0, 0);
+    HIPCHK(launch_slab_sum(ctx->slab.d(), ntp, (int)tiles_m, ntp, nullptr, ctx->s1.d(), s));
+    HIPCHK(launch_slab_sum(ctx->slab.d() + tiles_m * ntp, ntp, (int)tiles_m, ntp, nullptr,
+                           ctx->s2.d(), s));
+    HIPCHK(launch_pred_finalize(ctx->s1.d(), ctx->s2.d(), (int)nt, ctx->th.sn2 + ctx->th.sf2,
+                                ctx->mu.d(), ctx->var.d(), s));
+    HIPCHK(launch_score_sums(ctx->mu.d(), ctx->var.d(), ctx->yt.d(), (int)nt, ctx->ytr_mean,
+                             ctx->ytr_var, ctx->small.d(), s));
+  }
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, 6 * 8, hipMemcpyDeviceToHost, s));
+  if (mu) HIPCHK(hipMemcpyAsync(mu, ctx->mu.p, nt * 8, hipMemcpyDeviceToHost, s));
+  if (var) HIPCHK(hipMemcpyAsync(var, ctx->var.p, nt * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (sc) score_bundle(ctx->hsmall, (double)nt, sc);
+  return 0;
+}
+
+// ---------------------------------------------------------------------- FITC
+int gps_fitc_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n, int d,
+                      double ytr_mean, double ytr_var_unbiased, int64_t n_total) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(X && y && n > 0 && d >= 1 && d <= GPS_MAX_D && n_total >= n, "bad FITC training data");
+  ctx->fn = n;
+  ctx->fd = d;
+  ctx->fn_pad = pad_to(n);
+  ctx->fn_total = n_total;
+  ctx->f_ytr_mean = ytr_mean;
+  ctx->f_ytr_var = ytr_var_unbiased;
+  if (int rc = upload(ctx, ctx->fX, X, n, d, ctx->fn_pad)) return rc;
+  if (int rc = upload(ctx, ctx->fy, y, n, 1, ctx->fn_pad)) return rc;
+  ctx->f_data = true;
+  ctx->f_fitted = false;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_fitc_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t nt,
+                      int64_t nt_total) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->f_data, "gps_fitc_set_data first");
+  ARGCHK(Xt && nt >= 0 && nt_total >= nt, "bad FITC test data");
+  ctx->fnt = nt;
+  ctx->fnt_pad = pad_to(std::max<int64_t>(nt, 1));
+  ctx->fnt_total = nt_total;
+  if (int rc = upload(ctx, ctx->fXt, Xt, nt, ctx->fd, ctx->fnt_pad)) return rc;
+  std::vector<double> zeros;
+  if (!yt) zeros.assign(std::max<int64_t>(nt, 1), 0.0);
+  if (int rc = upload(ctx, ctx->fyt, yt ? yt : zeros.data(), nt, 1, ctx->fnt_pad)) return rc;
+  ctx->f_test = true;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->f_data, "gps_fitc_set_data first");
+  ARGCHK(Z && m > 0, "bad inducing points");
+  ctx->m = m;
+  ctx->m_pad = pad_to(m);
+  if (int rc = upload(ctx, ctx->Z, Z, m, ctx->fd, ctx->m_pad)) return rc;
+  ctx->f_z = true;
+  ctx->f_fitted = false;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
+                 double* mu_loo, double* var_loo) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->f_data && ctx->f_z, "gps_fitc_set_data / gps_fitc_set_inducing first");
+  if (int rc = set_theta(ctx, ctx->fth, GPS_ARD, theta, n_ell, ctx->fd)) return rc;
+  const Theta& th = ctx->fth;
+  const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
+  const int64_t tm = mp / GPS_TILE;
+  hipStream_t s = ctx->stream;
+  // buffers
+  HIPCHK(ensure(ctx->Kmm, (size_t)mp * mp * 8));
+  HIPCHK(ensure(ctx->Am, (size_t)mp * mp * 8));
+  if (ctx->lm_zeroed != (size_t)mp || ctx->Lm.cap < (size_t)mp * mp * 8) {
+    HIPCHK(ensure(ctx->Lm, (size_t)mp * mp * 8));
+    HIPCHK(ensure(ctx->Lb, (size_t)mp * mp * 8));
+    HIPCHK(hipMemsetAsync(ctx->Lm.p, 0, (size_t)mp * mp * 8, s));
+    HIPCHK(hipMemsetAsync(ctx->Lb.p, 0, (size_t)mp * mp * 8, s));
+    ctx->lm_zeroed = (size_t)mp;
+  }
+  HIPCHK(ensure(ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(mp) * 8)));
+  HIPCHK(ensure(ctx->ldm, mp * 8));
+  HIPCHK(ensure(ctx->ldb, mp * 8));
+  HIPCHK(ensure(ctx->Knm, (size_t)np * mp * 8));
+  HIPCHK(ensure(ctx->q, np * 8));
+  HIPCHK(ensure(ctx->lam, np * 8));
+  HIPCHK(ensure(ctx->ilam, np * 8));
+  HIPCHK(ensure(ctx->ys, np * 8));
+  HIPCHK(ensure(ctx->r, np * 8));
+  HIPCHK(ensure(ctx->g, np * 8));
+  HIPCHK(ensure(ctx->fmu_loo, np * 8));
+  HIPCHK(ensure(ctx->fvar_loo, np * 8));
+  HIPCHK(ensure(ctx->c, mp * 8));
+  HIPCHK(ensure(ctx->tvec, mp * 8));
+  const int64_t red_len = mp * mp + mp + 8;
+  HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
+  // split-K for the m×m SYRK over n rows: aim at ~2048 workgroups
+  const int64_t tiles_lower = tm * (tm + 1) / 2;
+  int ks = (int)std::max<int64_t>(1, std::min<int64_t>(np / GPS_TILE, 2048 / tiles_lower));
+  HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
+  const int64_t nchunk = (std::max(np, mp) + 255) / 256;
+  const int64_t fslab_len = std::max<int64_t>(tm * np, nchunk * mp * 2);
+  HIPCHK(ensure(ctx->fslab, (size_t)fslab_len * 8));
+  double* red = ctx->red.d();
+  double* Bacc = red;
+  double* bvec = red + mp * mp;
+  double* scal = red + mp * mp + mp;  // [Σlogλ, Σy²/λ, Σcrps, Σlogs]
+  double* sm = ctx->small.d();        // [logdet_m/2, logdet_b/2, bᵀc]
+  int rc;
+  if ((rc = reset_info(ctx))) return rc;
+  // --- replicated m×m part: K̃mm = K(Z,Z) + 1e-3 I (KF:36), Lm⁻¹
+  if ((rc = gram(ctx, "gram_kmm", ctx->Z.d(), (int)m, ctx->Z.d(), (int)m, ctx->fd, th, 1e-3, 0, 1,
+                 ctx->Kmm.d(), mp, (int)mp, (int)mp)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(ctx->Am.p, ctx->Kmm.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
+  if ((rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr)))
+    return rc;
+  HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
+  // --- this shard's rows
+  if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
+                 ctx->Knm.d(), mp, (int)np, (int)mp)))
+    return rc;
+  {  // q_i = ‖Lm⁻¹ k_i‖²
+    GemmParams p = gp0();
+    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lm.d(); p.ldb = mp;
+    p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+    p.out0 = ctx->fslab.d(); p.ld_out = np;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p))) return rc;
+    HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->q.d(), s));
+  }
+  {
+    Prof pr(ctx, "fitc_lambda", 0, 0);
+    HIPCHK(launch_fitc_lambda(ctx->q.d(), ctx->fy.d(), (int)n, (int)np, th.sf2, th.sn2,
+                              ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal, s));
+  }
+  {  // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs)
+    GemmParams p = gp0();
+    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
+    p.C = ctx->slabB.d(); p.ldc = mp; p.c_kslice_stride = mp * mp;
+    p.M = (int)mp; p.N = (int)mp; p.K = (int)np; p.kscale = ctx->ilam.d();
+    p.lower_out = 1; p.ksplit = ks;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+    Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * mp * mp);
+    HIPCHK(launch_sym_slab_sum(ctx->slabB.d(), mp * mp, ks, (int)mp, nullptr, Bacc, s));
+  }
+  {  // b_p = Kmnᵀ Λ⁻¹ y
+    Prof pr(ctx, "colred_b", 0, 8.0 * np * mp);
+    HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ctx->ys.d(), nullptr, bvec,
+                         nullptr, ctx->fslab.d(), s));
+  }
+  if (ctx->comm) {
+    Prof pr(ctx, "rccl_allreduce_B", 0, 8.0 * (mp * mp + mp + 2));
+    NCCLCHK(ncclAllReduce(red, red, (size_t)(mp * mp + mp + 2), ncclFloat64, ncclSum, ctx->comm, s));
+  }
+  // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
+  HIPCHK(launch_sym_slab_sum(Bacc, 0, 1, (int)mp, ctx->Kmm.d(), ctx->Am.d(), s));
+  if ((rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr)))
+    return rc;
+  HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
+  {  // c = Lb⁻ᵀ Lb⁻¹ b
+    Prof pr(ctx, "fitc_c", 0, 0);
+    HIPCHK(launch_gemv_lower(ctx->Lb.d(), mp, bvec, ctx->tvec.d(), (int)mp, s));
+    HIPCHK(launch_colred(ctx->Lb.d(), mp, (int)mp, (int)mp, 1, ctx->tvec.d(), nullptr, ctx->c.d(),
+                         nullptr, ctx->fslab.d(), s));
+    HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
+  }
+  {  // r_i = ‖Lb⁻¹ k_i‖²
+    GemmParams p = gp0();
+    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp;
+    p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+    p.out0 = ctx->fslab.d(); p.ld_out = np;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p))) return rc;
+    HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->r.d(), s));
+  }
+  {
+    Prof pr(ctx, "fitc_loo", 0, 8.0 * np * mp);
+    HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, ctx->c.d(), ctx->g.d(), (int)np, (int)mp, s));
+    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n,
+                           ctx->fmu_loo.d(), ctx->fvar_loo.d(), scal + 2, s));
+  }
+  if (ctx->comm) NCCLCHK(ncclAllReduce(scal + 2, scal + 2, 2, ncclFloat64, ncclSum, ctx->comm, s));
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, scal, 4 * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(ctx->hsmall + 4, sm, 3 * 8, hipMemcpyDeviceToHost, s));
+  if ((rc = check_info(ctx))) return rc;
+  const double* h = ctx->hsmall;
+  const double N = (double)ctx->fn_total;
+  const double logdet = h[0] + 2.0 * h[5] - 2.0 * h[4];
+  const double quad = h[1] - h[6];
+  if (obj) {
+    obj[GPS_OBJ_NLML] = 0.5 * N * 1.83787706640934548356 + 0.5 * logdet + 0.5 * quad;
+    obj[GPS_OBJ_LOO_CRPS] = h[2] / N;
+    obj[GPS_OBJ_LOO_LOGS] = h[3] / N;
+    obj[GPS_OBJ_LOGDET] = logdet;
+    obj[GPS_OBJ_QUAD] = quad;
+  }
+  if (mu_loo) HIPCHK(hipMemcpyAsync(mu_loo, ctx->fmu_loo.p, n * 8, hipMemcpyDeviceToHost, s));
+  if (var_loo) HIPCHK(hipMemcpyAsync(var_loo, ctx->fvar_loo.p, n * 8, hipMemcpyDeviceToHost, s));
+  if (mu_loo || var_loo) HIPCHK(hipStreamSynchronize(s));
+  ctx->f_fitted = true;
+  return 0;
+}
+
+int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->f_fitted, "gps_fitc_fit first");
+  ARGCHK(ctx->f_test, "gps_fitc_set_test first");
+  const Theta& th = ctx->fth;
+  const int64_t nt = ctx->fnt, ntp = ctx->fnt_pad, m = ctx->m, mp = ctx->m_pad;
+  const int64_t tm = mp / GPS_TILE;
+  hipStream_t s = ctx->stream;
+  HIPCHK(ensure(ctx->Ksm, (size_t)ntp * mp * 8));
+  HIPCHK(ensure(ctx->qm, ntp * 8));
+  HIPCHK(ensure(ctx->qb, ntp * 8));
+  HIPCHK(ensure(ctx->fmu, ntp * 8));
+  HIPCHK(ensure(ctx->fvar, ntp * 8));
+  HIPCHK(ensure(ctx->fslab, std::max(ctx->fslab.cap, (size_t)tm * ntp * 8)));
+  double* sums = ctx->small.d() + 8;
+  int rc;
+  if ((rc = gram(ctx, "gram_ksm", ctx->fXt.d(), (int)nt, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
+                 ctx->Ksm.d(), mp, (int)ntp, (int)mp)))
+    return rc;
+  const double* Ls[2] = {ctx->Lm.d(), ctx->Lb.d()};
+  double* outs[2] = {ctx->qm.d(), ctx->qb.d()};
+  for (int w = 0; w < 2; ++w) {
+    GemmParams p = gp0();
+    p.A = ctx->Ksm.d(); p.lda = mp; p.B = Ls[w]; p.ldb = mp;
+    p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+    p.out0 = ctx->fslab.d(); p.ld_out = ntp;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p))) return rc;
+    HIPCHK(launch_slab_sum(ctx->fslab.d(), ntp, (int)tm, ntp, nullptr, outs[w], s));
+  }
+  {
+    Prof pr(ctx, "fitc_pred_finalize", 0, 8.0 * ntp * mp);
+    HIPCHK(launch_gemv_full(ctx->Ksm.d(), mp, ctx->c.d(), ctx->fmu.d(), (int)ntp, (int)mp, s));
+    HIPCHK(launch_fitc_pred_finalize(ctx->qm.d(), ctx->qb.d(), (int)nt, th.sn2 + th.sf2,
+                                     ctx->fvar.d(), s));
+    if (nt > 0)
+      HIPCHK(launch_score_sums(ctx->fmu.d(), ctx->fvar.d(), ctx->fyt.d(), (int)nt, ctx->f_ytr_mean,
+                               ctx->f_ytr_var, sums, s));
+    else
+      HIPCHK(hipMemsetAsync(sums, 0, 6 * 8, s));
+  }
+  if (ctx->comm) NCCLCHK(ncclAllReduce(sums, sums, 6, ncclFloat64, ncclSum, ctx->comm, s));
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, sums, 6 * 8, hipMemcpyDeviceToHost, s));
+  if (mu && nt) HIPCHK(hipMemcpyAsync(mu, ctx->fmu.p, nt * 8, hipMemcpyDeviceToHost, s));
+  if (var && nt) HIPCHK(hipMemcpyAsync(var, ctx->fvar.p, nt * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (sc) score_bundle(ctx->hsmall, (double)ctx->fnt_total, sc);
+  return 0;
+}
+
+// ---------------------------------------------------------------------- comm
+int gps_comm_unique_id(char uid[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  gps_ctx* ctx = nullptr;
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  memcpy(uid, &id, 128);
+  return 0;
+}
+
+int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(nranks >= 1 && rank >= 0 && rank < nranks && uid, "bad communicator arguments");
+  if (ctx->comm) {
+    ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ncclUniqueId id;
+  memcpy(&id, uid, 128);
+  NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return 0;
+}
+
+int gps_comm_destroy(gps_ctx* ctx) {
+  if (int rc = bind(ctx)) return rc;
+  if (ctx->comm) NCCLCHK(ncclCommDestroy(ctx->comm));
+  ctx->comm = nullptr;
+  ctx->nranks = 1;
+  ctx->rank = 0;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// Internal declarations shared by the gfx950 kernels and the C-ABI layer.
+// Everything here is float64; all device matrices are row-major and every
+// dimension handed to a kernel is padded to a multiple of GPS_TILE (128).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#define GPS_TILE 128
+#define GPS_MAX_D 64
+
+namespace gps {
+
+inline int64_t pad_to(int64_t n, int64_t t = GPS_TILE) { return (n + t - 1) / t * t; }
+
+// ---------------------------------------------------------------- kernel params
+struct GramParams {
+  const double* x;    // [n][d] raw features
+  const double* xp;   // [m][d]
+  double* out;        // [M_pad][ldo]
+  int64_t ldo;
+  int n, m;           // real rows / cols
+  int M, N;           // padded rows / cols written
+  int d;
+  double sf2;
+  double diag_add;    // added where i == j (real rows)
+  int lower;          // write only j <= i (tile-granular skip + element mask)
+  int pad_identity;   // 1.0 on the padded diagonal (i == j >= n)
+  double inv_ell[GPS_MAX_D];
+};
+
+enum Layout { LAY_N = 0, LAY_T = 1 };
+// triangular structure of an operand, expressed as a k-range restriction per tile
+enum Tri {
+  TRI_NONE = 0,
+  TRI_K_LE_I = 1,  // k < (ti+1)*128   (A lower, A[i][k] != 0 only for k <= i)
+  TRI_K_LE_J = 2,  // k < (tj+1)*128   (B = Lᵀ with L lower stored [j][k])
+  TRI_K_GE_J = 3,  // k >= tj*128      (B lower stored [k][j])
+  TRI_K_GE_I = 4,  // k >= ti*128      (A = Lᵀ with L lower stored [k][i])
+};
+enum Epi { EPI_STORE = 0, EPI_ROWSQ = 1, EPI_COLRED = 2 };
+
+struct GemmParams {
+  const double* A; int64_t lda;
+  const double* B; int64_t ldb;
+  double* C; int64_t ldc;
+  int64_t c_kslice_stride;   // split-K: slice s writes C + s*stride (beta must be 0)
+  int M, N, K;               // multiples of 128 (K: multiple of 16 after tri clipping)
+  double alpha, beta;
+  const double* kscale;      // optional per-k scale applied to A (length K)
+  const double* w;           // EPI_COLRED weights (length M)
+  double* out0; double* out1; int64_t ld_out;
+  int lower_out;             // enumerate only tiles with tj <= ti
+  int ksplit;                // number of K slices (grid.y)
+  int tri;
+  int tiles_m, tiles_n;
+};
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_gram(const GramParams& p, hipStream_t s);
+// C = alpha * op(A) op(B) + beta * C with the epilogue selected by `epi`
+hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& p, hipStream_t s);
+
+// diagonal 128×128 block: in-LDS Cholesky + triangular inverse.
+// Reads the lower triangle of A (lda), writes L⁻¹ (lower, upper zeroed) into
+// Linv (ldl) and log(L_ii) into logdiag[0..127]; sets *info (atomicMin) to the
+// 1-based global index of the first non-positive pivot.
+hipError_t launch_potrf_diag(const double* A, int64_t lda, double* Linv, int64_t ldl,
+                             double* Lout, int64_t ldlo, double* logdiag, int* info,
+                             int base_index, int n_real_in_block, hipStream_t s);
+
+// y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)
+hipError_t launch_gemv_lower(const double* L, int64_t ldl, const double* x, double* y,
+                             int n_pad, hipStream_t s);
+// y[i] = sum_k M[i][k] x[k], full rows
+hipError_t launch_gemv_full(const double* M, int64_t ldm, const double* x, double* y,
+                            int rows, int cols, hipStream_t s);
+// column reductions over rows i (tile-lower if lower != 0):
+//   s1[k] = sum_i M[i][k] w[i]   (if s1 != null)     s2[k] = sum_i M[i][k]^2 (if s2 != null)
+// rowscale (optional) multiplies M[i][k] by rowscale[i] before both sums.
+// Uses slab (>= nchunks*cols*2 doubles) and reduces into s1/s2.
+hipError_t launch_colred(const double* M, int64_t ldm, int rows, int cols, int lower,
+                         const double* w, const double* rowscale, double* s1, double* s2,
+                         double* slab, hipStream_t s);
+// out[j] = sum_{s < nslab} slab[s*ld + j] (+ init[j] if init), j < len
+hipError_t launch_slab_sum(const double* slab, int64_t ld, int nslab, int64_t len,
+                           const double* init, double* out, hipStream_t s);
+// sum of B slices into dst lower tiles + add (optional) base matrix; zero strict-upper tiles
+hipError_t launch_sym_slab_sum(const double* slab, int64_t slice_stride, int nslab, int M,
+                               const double* base, double* dst, hipStream_t s);
+
+// full-GP LOO finalize (one workgroup): see kernels_vec.hip
+hipError_t launch_full_loo(const double* y, const double* alpha, const double* dinv,
+                           const double* beta, const double* logdiag, int n,
+                           double* mu_loo, double* var_loo, double* obj, hipStream_t s);
+// predictive variance finalize + test-score partial sums
+hipError_t launch_pred_finalize(const double* s1, const double* s2, int nt, double base_var,
+                                double* mu, double* var, hipStream_t s);
+hipError_t launch_fitc_pred_finalize(const double* qm, const double* qb, int nt, double base_var,
+                                     double* var, hipStream_t s);
+// sums: [crps, logs, msll, sq_err, sq_err_trivial, cover]
+hipError_t launch_score_sums(const double* mu, const double* var, const double* y, int nt,
+                             double ytr_mean, double ytr_var, double* sums, hipStream_t s);
+// FITC: λ_i = sf2 − q_i + σ² (real rows), 1 on pad rows; inv_lam = 1/λ; ys = y/λ;
+// scalars: [Σ log λ, Σ y²/λ]
+hipError_t launch_fitc_lambda(const double* q, const double* y, int n, int n_pad, double sf2,
+                              double sn2, double* lam, double* inv_lam, double* ys,
+                              double* scal, hipStream_t s);
+// FITC LOO sums: d = 1/λ − r/λ², α = (y − g)/λ → μ, σ²; sums [Σ crps, Σ logs]
+hipError_t launch_fitc_loo(const double* y, const double* lam, const double* r, const double* g,
+                           int n, double* mu_loo, double* var_loo, double* sums, hipStream_t s);
+// small dense triangular mat-vec on the device: y = op(L) x with L lower (n_pad)
+hipError_t launch_trmv_lower(const double* L, int64_t ldl, const double* x, double* y,
+                             int n_pad, int trans, hipStream_t s);
+hipError_t launch_dot(const double* a, const double* b, int n, double* out, hipStream_t s);
+// dst (rows_pad × cols_pad) = src zero-padded; pad_identity puts 1 on the padded
+// diagonal (embedding an SPD matrix as diag(A, I))
+hipError_t launch_pad_copy(const double* src, int64_t lds, double* dst, int64_t ldd, int rows,
+                           int cols, int rows_pad, int cols_pad, int pad_identity, hipStream_t s);
+
+}  // namespace gps

@@ -1,0 +1,107 @@
+// Fused ARD / RBF Gram build for gfx950 (replaces ARD KF:7-23 and rbf SD:8-21).
+//
+//   out[i][j] = sf2 * exp(-0.5 * sum_k ((x_ik - x'_jk) / l_k)^2)  (+ diag_add if i == j)
+//
+// The reference builds this from ~5 eager n×m temporaries (mm, two bmm, subtract,
+// scale, exp).  Here one pass writes each fp64 output exactly once: the kernel is
+// bound by HBM write bandwidth (8 B per element; roofline "hbm").
+//
+// Tile: 32 rows × 128 columns per 256-thread workgroup.  Each lane owns two
+// adjacent columns (one 16-byte store per row), each wave walks 8 rows.  The
+// scaled features of the tile's 128 columns live in LDS transposed [k][col] so a
+// lane reads its two columns with one conflict-free ds_read_b128 per feature;
+// the row features are broadcast reads.  With `lower`, tiles strictly above the
+// diagonal are skipped and elements with j > i are not written (the Cholesky
+// reads only the lower triangle).  Rows >= n / columns >= m are padding: they
+// get 0, or 1 on the diagonal when pad_identity is set, so the padded SPD
+// matrix is diag(A, I) and its factor/inverse are diag(L, I) / diag(L⁻¹, I).
+#include "gps_internal.h"
+
+namespace gps {
+
+constexpr int GR_ROWS = 32;
+constexpr int GR_COLS = 128;
+
+template <int D>
+__global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
+  __shared__ __attribute__((aligned(16))) double xs_col[(D ? D : GPS_MAX_D) * GR_COLS];
+  __shared__ double xs_row[GR_ROWS * (D ? D : GPS_MAX_D)];
+  const int d = D ? D : p.d;
+  const int tiles_x = p.N / GR_COLS;
+  const int bx = blockIdx.x % tiles_x;
+  const int by = blockIdx.x / tiles_x;
+  const int c0 = bx * GR_COLS, r0 = by * GR_ROWS;
+  if (p.lower && c0 > r0 + GR_ROWS - 1) return;
+  const int tid = threadIdx.x;
+
+  for (int e = tid; e < GR_COLS * d; e += 256) {
+    const int j = e / d, k = e - j * d;
+    const int gj = c0 + j;
+    xs_col[k * GR_COLS + j] = gj < p.m ? p.xp[(int64_t)gj * d + k] * p.inv_ell[k] : 0.0;
+  }
+  for (int e = tid; e < GR_ROWS * d; e += 256) {
+    const int i = e / d, k = e - i * d;
+    const int gi = r0 + i;
+    xs_row[i * d + k] = gi < p.n ? p.x[(int64_t)gi * d + k] * p.inv_ell[k] : 0.0;
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int jl = 2 * lane;
+  const int gj = c0 + jl;
+  const bool colpad0 = gj >= p.m, colpad1 = gj + 1 >= p.m;
+
+#pragma unroll 2
+  for (int rr = wave; rr < GR_ROWS; rr += 4) {
+    const int gi = r0 + rr;
+    double a0 = 0.0, a1 = 0.0;
+    if constexpr (D > 0) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double xr = xs_row[rr * D + k];
+        const double2 xc = *reinterpret_cast<const double2*>(&xs_col[k * GR_COLS + jl]);
+        const double e0 = xr - xc.x, e1 = xr - xc.y;
+        a0 = fma(e0, e0, a0);
+        a1 = fma(e1, e1, a1);
+      }
+    } else {
+      for (int k = 0; k < d; ++k) {
+        const double xr = xs_row[rr * d + k];
+        const double2 xc = *reinterpret_cast<const double2*>(&xs_col[k * GR_COLS + jl]);
+        const double e0 = xr - xc.x, e1 = xr - xc.y;
+        a0 = fma(e0, e0, a0);
+        a1 = fma(e1, e1, a1);
+      }
+    }
+    double v0 = p.sf2 * exp(-0.5 * a0);
+    double v1 = p.sf2 * exp(-0.5 * a1);
+    const bool rowpad = gi >= p.n;
+    if (gi == gj) v0 += p.diag_add;
+    if (gi == gj + 1) v1 += p.diag_add;
+    if (rowpad || colpad0) v0 = (p.pad_identity && gi == gj) ? 1.0 : 0.0;
+    if (rowpad || colpad1) v1 = (p.pad_identity && gi == gj + 1) ? 1.0 : 0.0;
+    double* dst = p.out + (int64_t)gi * p.ldo + gj;
+    if (!p.lower || gj + 1 <= gi) {
+      *reinterpret_cast<double2*>(dst) = make_double2(v0, v1);
+    } else if (gj <= gi) {
+      dst[0] = v0;
+    }
+  }
+}
+
+hipError_t launch_gram(const GramParams& p, hipStream_t s) {
+  if (p.d < 1 || p.d > GPS_MAX_D || p.M % GR_ROWS || p.N % GR_COLS || (p.ldo & 1))
+    return hipErrorInvalidValue;
+  const int64_t blocks = (int64_t)(p.M / GR_ROWS) * (p.N / GR_COLS);
+  if (blocks == 0) return hipSuccess;
+  dim3 grid((unsigned)blocks), block(256);
+  switch (p.d) {
+    case 1: hipLaunchKernelGGL(gram_kernel<1>, grid, block, 0, s, p); break;
+    case 8: hipLaunchKernelGGL(gram_kernel<8>, grid, block, 0, s, p); break;
+    case 16: hipLaunchKernelGGL(gram_kernel<16>, grid, block, 0, s, p); break;
+    default: hipLaunchKernelGGL(gram_kernel<0>, grid, block, 0, s, p); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace gps

@@ -1,0 +1,407 @@
+// Bandwidth / latency-bound kernels around the factorisation:
+//   β = L⁻¹y (row GEMV), α = L⁻ᵀβ and diag(A⁻¹) = colsum(L⁻¹∘L⁻¹) (one fused column
+//   pass), the LOO closed form (R&W eq. 5.12, KF:241-244), the FITC Λ and LOO
+//   terms (K20:225-232 restated), and the scoring-rule sums crps / logs /
+//   trivial_loss / SMSE / MSE / ±2σ coverage (KF:52-68, 110-134, 276-292).
+// All reductions are fixed-order trees (no atomics) so results are bitwise
+// reproducible run to run.
+#include "gps_internal.h"
+
+namespace gps {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// block-wide sum of NV values per thread; result valid in every thread
+template <int NV>
+__device__ void block_sum(double (&v)[NV], double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = wave_sum(v[q]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) sh[q * 16 + wave] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += sh[q * 16 + w];
+    v[q] = t;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double crps_term(double m, double c, double y) {
+  const double s = sqrt(c);
+  const double z = (y - m) / s;
+  const double cdf = 0.5 * (1.0 + erf(z * 0.70710678118654752440));
+  const double pdf = 0.39894228040143267794 * exp(-z * z * 0.5);
+  return s * (z * (2.0 * cdf - 1.0) + 2.0 * pdf - 0.56418958354775628695);
+}
+__device__ __forceinline__ double logs_term(double m, double c, double y) {
+  const double e = y - m;
+  return e * e / (2.0 * c) + log(sqrt(c)) + 0.91893853320467274178;
+}
+
+// ------------------------------------------------------------------ GEMV rows
+// one wave per row, 16-byte loads; tile-lower: k < (i/128 + 1)*128
+__global__ __launch_bounds__(256) void gemv_rows_kernel(const double* __restrict__ M, int64_t ldm,
+                                                        const double* __restrict__ x,
+                                                        double* __restrict__ y, int rows, int cols,
+                                                        int lower) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int kend = lower ? min(cols, (row / GPS_TILE + 1) * GPS_TILE) : cols;
+  const double* r = M + (int64_t)row * ldm;
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 2 * lane; k < kend; k += 128) {
+    const double2 v = *reinterpret_cast<const double2*>(r + k);
+    const double2 xv = *reinterpret_cast<const double2*>(x + k);
+    s0 = fma(v.x, xv.x, s0);
+    s1 = fma(v.y, xv.y, s1);
+  }
+  const double s = wave_sum(s0 + s1);
+  if (lane == 0) y[row] = s;
+}
+
+hipError_t launch_gemv_lower(const double* L, int64_t ldl, const double* x, double* y, int n_pad,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(gemv_rows_kernel, dim3((n_pad + 3) / 4), dim3(256), 0, s, L, ldl, x, y, n_pad,
+                     n_pad, 1);
+  return hipGetLastError();
+}
+hipError_t launch_gemv_full(const double* M, int64_t ldm, const double* x, double* y, int rows,
+                            int cols, hipStream_t s) {
+  if (cols & 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemv_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, M, ldm, x, y, rows,
+                     cols, 0);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- column reductions
+constexpr int CR_ROWS = 256;  // rows per chunk
+constexpr int CR_COLS = 512;  // columns per block (2 per thread)
+
+__global__ __launch_bounds__(256) void colred_kernel(const double* __restrict__ M, int64_t ldm,
+                                                     int rows, int cols, int lower,
+                                                     const double* __restrict__ w,
+                                                     const double* __restrict__ rowscale,
+                                                     double* __restrict__ slab1,
+                                                     double* __restrict__ slab2) {
+  const int c = blockIdx.x * CR_COLS + 2 * threadIdx.x;
+  const int chunk = blockIdx.y;
+  if (c >= cols) return;
+  int r0 = chunk * CR_ROWS, r1 = min(rows, r0 + CR_ROWS);
+  if (lower) r0 = max(r0, (c / GPS_TILE) * GPS_TILE);
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  for (int r = r0; r < r1; ++r) {
+    double2 v = *reinterpret_cast<const double2*>(M + (int64_t)r * ldm + c);
+    if (rowscale) {
+      const double sc = rowscale[r];
+      v.x *= sc;
+      v.y *= sc;
+    }
+    if (slab1) {
+      const double wr = w[r];
+      a0 = fma(v.x, wr, a0);
+      a1 = fma(v.y, wr, a1);
+    }
+    b0 = fma(v.x, v.x, b0);
+    b1 = fma(v.y, v.y, b1);
+  }
+  const int64_t o = (int64_t)chunk * cols + c;
+  if (slab1) *reinterpret_cast<double2*>(slab1 + o) = make_double2(a0, a1);
+  if (slab2) *reinterpret_cast<double2*>(slab2 + o) = make_double2(b0, b1);
+}
+
+__global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict__ slab, int64_t ld,
+                                                       int nslab, int64_t len,
+                                                       const double* __restrict__ init,
+                                                       double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= len) return;
+  double s = init ? init[j] : 0.0;
+  for (int q = 0; q < nslab; ++q) s += slab[(int64_t)q * ld + j];
+  out[j] = s;
+}
+
+hipError_t launch_slab_sum(const double* slab, int64_t ld, int nslab, int64_t len,
+                           const double* init, double* out, hipStream_t s) {
+  if (len <= 0) return hipSuccess;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, slab,
+                     ld, nslab, len, init, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_colred(const double* M, int64_t ldm, int rows, int cols, int lower,
+                         const double* w, const double* rowscale, double* s1, double* s2,
+                         double* slab, hipStream_t s) {
+  if ((cols & 1) || (ldm & 1)) return hipErrorInvalidValue;
+  const int nchunk = (rows + CR_ROWS - 1) / CR_ROWS;
+  double* slab1 = s1 ? slab : nullptr;
+  double* slab2 = s2 ? slab + (int64_t)nchunk * cols : nullptr;
+  hipLaunchKernelGGL(colred_kernel, dim3((cols + CR_COLS - 1) / CR_COLS, nchunk), dim3(256), 0, s,
+                     M, ldm, rows, cols, lower, w, rowscale, slab1, slab2);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (s1 && (e = launch_slab_sum(slab1, cols, nchunk, cols, nullptr, s1, s)) != hipSuccess) return e;
+  if (s2 && (e = launch_slab_sum(slab2, cols, nchunk, cols, nullptr, s2, s)) != hipSuccess) return e;
+  return hipSuccess;
+}
+
+// sum split-K slabs of a symmetric M×M accumulator; tile-lower kept, strict-upper
+// tiles zeroed (so the buffer can be all-reduced / factorised as is)
+__global__ __launch_bounds__(256) void sym_slab_sum_kernel(const double* __restrict__ slab,
+                                                           int64_t stride, int nslab, int M,
+                                                           const double* __restrict__ base,
+                                                           double* __restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)M * M) return;
+  const int i = (int)(e / M), j = (int)(e - (int64_t)i * M);
+  double v = 0.0;
+  if (j / GPS_TILE <= i / GPS_TILE) {
+    if (base) v = base[e];
+    for (int q = 0; q < nslab; ++q) v += slab[(int64_t)q * stride + e];
+  }
+  dst[e] = v;
+}
+
+hipError_t launch_sym_slab_sum(const double* slab, int64_t slice_stride, int nslab, int M,
+                               const double* base, double* dst, hipStream_t s) {
+  const int64_t tot = (int64_t)M * M;
+  hipLaunchKernelGGL(sym_slab_sum_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                     slab, slice_stride, nslab, M, base, dst);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ full-GP LOO
+// obj: [nlml, loo_crps, loo_logs, logdet, quad]; logdiag/beta over n_pad (pad = 0)
+__global__ __launch_bounds__(1024) void full_loo_kernel(const double* __restrict__ y,
+                                                        const double* __restrict__ alpha,
+                                                        const double* __restrict__ dinv,
+                                                        const double* __restrict__ beta,
+                                                        const double* __restrict__ logdiag, int n,
+                                                        int n_pad, double* __restrict__ mu_loo,
+                                                        double* __restrict__ var_loo,
+                                                        double* __restrict__ obj) {
+  __shared__ double sh[4 * 16];
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < n_pad; i += blockDim.x) {
+    v[2] += logdiag[i];
+    v[3] = fma(beta[i], beta[i], v[3]);
+    if (i < n) {
+      const double d = dinv[i];
+      const double m = y[i] - alpha[i] / d;
+      const double c = 1.0 / d;
+      mu_loo[i] = m;
+      var_loo[i] = c;
+      v[0] += crps_term(m, c, y[i]);
+      v[1] += logs_term(m, c, y[i]);
+    }
+  }
+  block_sum<4>(v, sh);
+  if (threadIdx.x == 0) {
+    const double logdet = 2.0 * v[2], quad = v[3];
+    obj[0] = 0.5 * n * 1.83787706640934548356 + 0.5 * logdet + 0.5 * quad;
+    obj[1] = v[0] / n;
+    obj[2] = v[1] / n;
+    obj[3] = logdet;
+    obj[4] = quad;
+  }
+}
+
+hipError_t launch_full_loo(const double* y, const double* alpha, const double* dinv,
+                           const double* beta, const double* logdiag, int n, double* mu_loo,
+                           double* var_loo, double* obj, hipStream_t s) {
+  const int n_pad = (int)pad_to(n);
+  hipLaunchKernelGGL(full_loo_kernel, dim3(1), dim3(1024), 0, s, y, alpha, dinv, beta, logdiag, n,
+                     n_pad, mu_loo, var_loo, obj);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------- predictive
+__global__ __launch_bounds__(256) void pred_finalize_kernel(const double* __restrict__ s1,
+                                                            const double* __restrict__ s2, int nt,
+                                                            double base_var, double* __restrict__ mu,
+                                                            double* __restrict__ var) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= nt) return;
+  mu[j] = s1[j];
+  var[j] = base_var - s2[j];
+}
+hipError_t launch_pred_finalize(const double* s1, const double* s2, int nt, double base_var,
+                                double* mu, double* var, hipStream_t s) {
+  hipLaunchKernelGGL(pred_finalize_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, s1, s2, nt,
+                     base_var, mu, var);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void fitc_pred_finalize_kernel(const double* __restrict__ qm,
+                                                                 const double* __restrict__ qb,
+                                                                 int nt, double base_var,
+                                                                 double* __restrict__ var) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= nt) return;
+  var[j] = base_var - qm[j] + qb[j];
+}
+hipError_t launch_fitc_pred_finalize(const double* qm, const double* qb, int nt, double base_var,
+                                     double* var, hipStream_t s) {
+  hipLaunchKernelGGL(fitc_pred_finalize_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, qm, qb, nt,
+                     base_var, var);
+  return hipGetLastError();
+}
+
+// sums: [Σcrps, Σlogs, Σmsll, Σ(μ−y)², Σ(ȳtr−y)², Σcover]  (KF:276-292, 110-134)
+__global__ __launch_bounds__(1024) void score_sums_kernel(const double* __restrict__ mu,
+                                                          const double* __restrict__ var,
+                                                          const double* __restrict__ y, int nt,
+                                                          double ytr_mean, double ytr_var,
+                                                          double* __restrict__ sums) {
+  __shared__ double sh[6 * 16];
+  double v[6] = {0, 0, 0, 0, 0, 0};
+  const double triv_c = 0.5 * log(6.28318530717958647692 * ytr_var);
+  for (int j = threadIdx.x; j < nt; j += blockDim.x) {
+    const double m = mu[j], c = var[j], t = y[j];
+    v[0] += crps_term(m, c, t);
+    const double ls = logs_term(m, c, t);
+    v[1] += ls;
+    const double e0 = t - ytr_mean;
+    v[2] += ls - (triv_c + e0 * e0 / (2.0 * ytr_var));
+    v[3] += (m - t) * (m - t);
+    v[4] += e0 * e0;
+    const double sd = sqrt(c);
+    v[5] += ((m + 2.0 * sd - t) > 0.0 && (t - (m - 2.0 * sd)) > 0.0) ? 1.0 : 0.0;
+  }
+  block_sum<6>(v, sh);
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 6; ++q) sums[q] = v[q];
+}
+hipError_t launch_score_sums(const double* mu, const double* var, const double* y, int nt,
+                             double ytr_mean, double ytr_var, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(score_sums_kernel, dim3(1), dim3(1024), 0, s, mu, var, y, nt, ytr_mean,
+                     ytr_var, sums);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------- FITC
+__global__ __launch_bounds__(1024) void fitc_lambda_kernel(const double* __restrict__ q,
+                                                           const double* __restrict__ y, int n,
+                                                           int n_pad, double sf2, double sn2,
+                                                           double* __restrict__ lam,
+                                                           double* __restrict__ inv_lam,
+                                                           double* __restrict__ ys,
+                                                           double* __restrict__ scal) {
+  __shared__ double sh[2 * 16];
+  double v[2] = {0.0, 0.0};
+  for (int i = threadIdx.x; i < n_pad; i += blockDim.x) {
+    if (i < n) {
+      const double l = sf2 - q[i] + sn2;  // G = diag(K_ff − Q_ff + σ²I), K20:225-228
+      const double il = 1.0 / l;
+      lam[i] = l;
+      inv_lam[i] = il;
+      ys[i] = y[i] * il;
+      v[0] += log(l);
+      v[1] = fma(y[i] * y[i], il, v[1]);
+    } else {
+      lam[i] = 1.0;
+      inv_lam[i] = 0.0;  // padded rows carry no weight in B = Kmnᵀ Λ⁻¹ Knm
+      ys[i] = 0.0;
+    }
+  }
+  block_sum<2>(v, sh);
+  if (threadIdx.x == 0) {
+    scal[0] = v[0];
+    scal[1] = v[1];
+  }
+}
+hipError_t launch_fitc_lambda(const double* q, const double* y, int n, int n_pad, double sf2,
+                              double sn2, double* lam, double* inv_lam, double* ys, double* scal,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(fitc_lambda_kernel, dim3(1), dim3(1024), 0, s, q, y, n, n_pad, sf2, sn2, lam,
+                     inv_lam, ys, scal);
+  return hipGetLastError();
+}
+
+// sums: [Σcrps, Σlogs] over this shard's rows
+__global__ __launch_bounds__(1024) void fitc_loo_kernel(const double* __restrict__ y,
+                                                        const double* __restrict__ lam,
+                                                        const double* __restrict__ r,
+                                                        const double* __restrict__ g, int n,
+                                                        double* __restrict__ mu_loo,
+                                                        double* __restrict__ var_loo,
+                                                        double* __restrict__ sums) {
+  __shared__ double sh[2 * 16];
+  double v[2] = {0.0, 0.0};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double il = 1.0 / lam[i];
+    const double d = il - r[i] * il * il;   // diag((Q+Λ)⁻¹), Woodbury
+    const double a = (y[i] - g[i]) * il;    // ((Q+Λ)⁻¹ y)_i
+    const double m = y[i] - a / d;          // K20:231
+    const double c = 1.0 / d;               // K20:232
+    mu_loo[i] = m;
+    var_loo[i] = c;
+    v[0] += crps_term(m, c, y[i]);
+    v[1] += logs_term(m, c, y[i]);
+  }
+  block_sum<2>(v, sh);
+  if (threadIdx.x == 0) {
+    sums[0] = v[0];
+    sums[1] = v[1];
+  }
+}
+hipError_t launch_fitc_loo(const double* y, const double* lam, const double* r, const double* g,
+                           int n, double* mu_loo, double* var_loo, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(fitc_loo_kernel, dim3(1), dim3(1024), 0, s, y, lam, r, g, n, mu_loo, var_loo,
+                     sums);
+  return hipGetLastError();
+}
+
+// --------------------------------------------------------------------- small
+__global__ __launch_bounds__(1024) void dot_kernel(const double* __restrict__ a,
+                                                   const double* __restrict__ b, int n,
+                                                   double* __restrict__ out) {
+  __shared__ double sh[16];
+  double v[1] = {0.0};
+  for (int i = threadIdx.x; i < n; i += blockDim.x) v[0] += b ? a[i] * b[i] : a[i];
+  block_sum<1>(v, sh);
+  if (threadIdx.x == 0) out[0] = v[0];
+}
+hipError_t launch_dot(const double* a, const double* b, int n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(dot_kernel, dim3(1), dim3(1024), 0, s, a, b, n, out);
+  return hipGetLastError();
+}
+
+// dst (rows_pad × cols_pad, ldd) = src (rows × cols, lds) zero-padded; identity on
+// the padded diagonal when pad_identity (used to embed a user SPD matrix)
+__global__ __launch_bounds__(256) void pad_copy_kernel(const double* __restrict__ src, int64_t lds,
+                                                       double* __restrict__ dst, int64_t ldd, int rows,
+                                                       int cols, int rows_pad, int cols_pad,
+                                                       int pad_identity) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)rows_pad * cols_pad) return;
+  const int i = (int)(e / cols_pad), j = (int)(e - (int64_t)i * cols_pad);
+  double v;
+  if (i < rows && j < cols) v = src[(int64_t)i * lds + j];
+  else v = (pad_identity && i == j) ? 1.0 : 0.0;
+  dst[(int64_t)i * ldd + j] = v;
+}
+hipError_t launch_pad_copy(const double* src, int64_t lds, double* dst, int64_t ldd, int rows,
+                           int cols, int rows_pad, int cols_pad, int pad_identity, hipStream_t s) {
+  const int64_t tot = (int64_t)rows_pad * cols_pad;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src, lds,
+                     dst, ldd, rows, cols, rows_pad, cols_pad, pad_identity);
+  return hipGetLastError();
+}
+
+hipError_t launch_trmv_lower(const double* L, int64_t ldl, const double* x, double* y, int n_pad,
+                             int trans, hipStream_t s) {
+  if (!trans) return launch_gemv_lower(L, ldl, x, y, n_pad, s);
+  return hipErrorInvalidValue;  // transposed form goes through launch_colred (needs a slab)
+}
+
+}  // namespace gps

@@ -1,0 +1,15 @@
+"""gpscore — MI355X (gfx950) GP-regression hot path: Gram build, Cholesky /
+log-determinant / solves, LOO and test-set CRPS / log-score, for the full GP and
+the FITC sparse GP (Woodbury form, rows sharded over GPUs with RCCL).
+
+Drop-in layers:
+  * ``gpscore.compat``  — the reference scripts' helper functions, same names;
+  * ``gpscore.GP``      — fit / predict / score on numpy arrays;
+  * ``gpscore.dist``    — one process per GPU, FITC row sharding;
+  * ``gpscore._lib``    — the ctypes binding of libgpscore.so (include/gpscore.h).
+"""
+from ._lib import (Context, GpsError, NotPositiveDefinite, default_context, load,  # noqa: F401
+                   OBJ_NAMES, SCORE_NAMES)
+from .gp import GP, FitResult, fit, pack_theta, score  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,168 @@
+"""ctypes binding of libgpscore.so (C-ABI declared in include/gpscore.h).
+
+This is the reference-side binding a maintainer adds under the reference
+scripts: plain pointers and sizes, no torch types.  There is no
+CPU fallback anywhere in this package: if the library is missing or no HIP
+device is present, loading / context creation raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
+
+GPS_ARD, GPS_RBF = 0, 1
+GPS_FULL, GPS_LOWER = 0, 1
+OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
+SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
+
+_c_int, _c_i64, _c_dbl, _c_vp, _c_cp = (ctypes.c_int, ctypes.c_int64, ctypes.c_double,
+                                        ctypes.c_void_p, ctypes.c_char_p)
+_P = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); every symbol include/gpscore.h declares
+SIGNATURES = {
+    "gps_version": (_c_int, []),
+    "gps_ctx_create": (_c_int, [_c_int, ctypes.POINTER(_c_vp)]),
+    "gps_ctx_destroy": (_c_int, [_c_vp]),
+    "gps_last_error": (_c_cp, [_c_vp]),
+    "gps_ctx_set_stream": (_c_int, [_c_vp, _c_vp]),
+    "gps_ctx_stream": (_c_vp, [_c_vp]),
+    "gps_ctx_synchronize": (_c_int, [_c_vp]),
+    "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
+    "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
+    "gps_gram": (_c_int, [_c_vp, _c_int, _P, _c_i64, _P, _c_i64, _c_int, _c_dbl, _P, _c_int,
+                          _c_dbl, _c_int, _P]),
+    "gps_potrf": (_c_int, [_c_vp, _c_i64, _P, _c_i64, _P]),
+    "gps_potrs": (_c_int, [_c_vp, _c_i64, _c_i64, _P, _c_i64, _P, _c_i64, _P, _c_i64]),
+    "gps_diag_inv": (_c_int, [_c_vp, _c_i64, _P, _c_i64, _P]),
+    "gps_gemm": (_c_int, [_c_vp, _c_int, _c_int, _c_i64, _c_i64, _c_i64, _c_dbl, _P, _c_i64, _P,
+                          _c_i64, _c_dbl, _P, _c_i64]),
+    "gps_scores": (_c_int, [_c_vp, _P, _P, _P, _c_i64, _c_dbl, _c_dbl, _P]),
+    "gps_full_set_data": (_c_int, [_c_vp, _P, _P, _c_i64, _c_int]),
+    "gps_full_set_test": (_c_int, [_c_vp, _P, _P, _c_i64]),
+    "gps_full_fit": (_c_int, [_c_vp, _c_int, _P, _c_int, _P, _P, _P]),
+    "gps_full_predict": (_c_int, [_c_vp, _P, _P, _P]),
+    "gps_fitc_set_data": (_c_int, [_c_vp, _P, _P, _c_i64, _c_int, _c_dbl, _c_dbl, _c_i64]),
+    "gps_fitc_set_test": (_c_int, [_c_vp, _P, _P, _c_i64, _c_i64]),
+    "gps_fitc_set_inducing": (_c_int, [_c_vp, _P, _c_i64]),
+    "gps_fitc_fit": (_c_int, [_c_vp, _P, _c_int, _P, _P, _P]),
+    "gps_fitc_predict": (_c_int, [_c_vp, _P, _P, _P]),
+    "gps_comm_unique_id": (_c_int, [_c_cp]),
+    "gps_comm_init": (_c_int, [_c_vp, _c_int, _c_int, _c_cp]),
+    "gps_comm_destroy": (_c_int, [_c_vp]),
+}
+
+_lib = None
+
+
+class GpsError(RuntimeError):
+    """A HIP / RCCL / argument error reported by libgpscore (status < 0)."""
+
+
+class NotPositiveDefinite(GpsError):
+    """Cholesky hit a non-positive pivot (status > 0), as torch.potrf raises
+    RuntimeError (the reference catches it at KF:726 / K20:784)."""
+
+    def __init__(self, info, msg):
+        super().__init__(msg)
+        self.info = info
+
+
+def load():
+    """Load libgpscore.so once; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libgpscore.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C <pkg>/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(a):
+    """float64 pointer of a C-contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(_P)
+
+
+def f64(a, ndim=None):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if ndim == 2 and a.ndim == 1:
+        a = a.reshape(-1, 1)
+    return a
+
+
+class Context:
+    """One device + one HIP stream + the device-resident buffers of the hot path."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = _c_vp()
+        rc = self.lib.gps_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise GpsError(f"gps_ctx_create(device={device}) failed: "
+                           f"{self.lib.gps_last_error(None).decode()}")
+        self.h = h
+        self.device = device
+
+    def check(self, rc, what):
+        if rc == 0:
+            return
+        msg = self.lib.gps_last_error(self.h).decode()
+        if rc > 0:
+            raise NotPositiveDefinite(rc, f"{what}: {msg}")
+        raise GpsError(f"{what} failed ({rc}): {msg}")
+
+    def call(self, name, *args):
+        self.check(getattr(self.lib, name)(self.h, *args), name)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gps_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- profiling
+    def prof(self, on=True):
+        self.call("gps_prof_enable", 1 if on else 0)
+
+    def prof_collect(self):
+        import json
+        buf = ctypes.create_string_buffer(1 << 16)
+        self.call("gps_prof_collect", buf, len(buf))
+        return json.loads(buf.value.decode())
+
+    def synchronize(self):
+        self.call("gps_ctx_synchronize")
+
+    def set_stream(self, stream_handle):
+        self.call("gps_ctx_set_stream", _c_vp(stream_handle))
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        dev = int(os.environ.get("GPSCORE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        _default_ctx = Context(dev)
+    return _default_ctx

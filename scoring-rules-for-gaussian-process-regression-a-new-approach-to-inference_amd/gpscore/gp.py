@@ -1,0 +1,166 @@
+"""High-level facade: fit / predict / score on numpy arrays.
+
+    gp = gpscore.GP()                             # one device context
+    res = gp.fit(X, y, theta)                     # full GP  (KF:239-245, 329-334, 416-424)
+    res = gp.fit(X, y, theta, kind="fitc", Z=Z)   # FITC     (K20:222-234, 329-340, 434-447)
+    mu, var = gp.predict(Xt)                      # cal_mean_and_cov / spgp_cal_mean_and_cov, diag
+    sc = gp.score(mu, var, yt, y)                 # crps, logs, trivial_loss, SMSE, MSE, coverage
+
+``theta = (log_sf2, log_ell, log_sn2)`` uses the reference's log-parameterisation
+(para_k, para_l, para_noise): ``log_ell`` is a scalar or a length-d vector
+(ARD, b = log ℓ, KF:8-12); with ``rbf=True`` it is log ℓ² (SD:8-21).
+
+Every number is computed by libgpscore.so on the GPU; there is no CPU path.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import GPS_ARD, GPS_RBF, OBJ_NAMES, SCORE_NAMES, f64, ptr
+
+
+def pack_theta(theta, d):
+    """[log_sf2, log_ell..., log_sn2] as the C-ABI expects; returns (array, n_ell)."""
+    log_sf2, log_ell, log_sn2 = theta
+    ell = np.atleast_1d(np.asarray(log_ell, dtype=np.float64)).ravel()
+    if ell.size not in (1, d):
+        raise ValueError(f"log_ell has {ell.size} entries, expected 1 or d={d}")
+    t = np.concatenate([[float(np.asarray(log_sf2).ravel()[0])], ell,
+                        [float(np.asarray(log_sn2).ravel()[0])]])
+    return np.ascontiguousarray(t), int(ell.size)
+
+
+@dataclass
+class FitResult:
+    kind: str
+    objectives: dict
+    mu_loo: np.ndarray | None = None
+    var_loo: np.ndarray | None = None
+    extra: dict = field(default_factory=dict)
+
+    def __getitem__(self, k):
+        return self.objectives[k]
+
+
+class GP:
+    """Device-resident GP hot path (one context = one GPU + one HIP stream)."""
+
+    def __init__(self, ctx: _lib.Context | None = None, device: int | None = None):
+        if ctx is None:
+            ctx = _lib.Context(device) if device is not None else _lib.default_context()
+        self.ctx = ctx
+        self.kind = None
+        self._X = self._Z = None
+        self._train_key = self._test_key = self._z_key = None
+        self.comm = None  # set by gpscore.dist.attach_comm
+        self.n_total = None
+        self.nt_total = None
+        self.ytr_stats = None  # (mean, unbiased var) over ALL ranks' training targets
+
+    # ------------------------------------------------------------------ data
+    def set_data(self, X, y, kind="full", Z=None, n_total=None, ytr_stats=None):
+        X, y = f64(X, 2), f64(y).ravel()
+        if X.shape[0] != y.size:
+            raise ValueError("X and y disagree on n")
+        n, d = X.shape
+        self.kind = kind
+        self._X, self._y = X, y
+        if kind == "full":
+            self.ctx.call("gps_full_set_data", ptr(X), ptr(y), n, d)
+        elif kind == "fitc":
+            self.n_total = n if n_total is None else int(n_total)
+            if ytr_stats is None:
+                ytr_stats = (float(y.mean()), float(y.var(ddof=1)) if n > 1 else 1.0)
+            self.ytr_stats = ytr_stats
+            self.ctx.call("gps_fitc_set_data", ptr(X), ptr(y), n, d, ytr_stats[0], ytr_stats[1],
+                          self.n_total)
+            if Z is not None:
+                self.set_inducing(Z)
+        else:
+            raise ValueError("kind must be 'full' or 'fitc'")
+        self._train_key = (id(X), X.shape)
+        return self
+
+    def set_inducing(self, Z):
+        Z = f64(Z, 2)
+        if self._X is not None and Z.shape[1] != self._X.shape[1]:
+            raise ValueError("Z and X disagree on d")
+        self._Z = Z
+        self.ctx.call("gps_fitc_set_inducing", ptr(Z), Z.shape[0])
+
+    def set_test(self, Xt, yt=None, nt_total=None):
+        Xt = f64(Xt, 2)
+        yt = None if yt is None else f64(yt).ravel()
+        nt = Xt.shape[0]
+        if self.kind == "full":
+            self.ctx.call("gps_full_set_test", ptr(Xt), ptr(yt), nt)
+        else:
+            self.nt_total = nt if nt_total is None else int(nt_total)
+            self.ctx.call("gps_fitc_set_test", ptr(Xt), ptr(yt), nt, self.nt_total)
+        self._nt = nt
+        self._has_yt = yt is not None
+
+    # ------------------------------------------------------------------- fit
+    def fit(self, X=None, y=None, theta=(0.0, 0.0, 0.0), kind="full", Z=None, rbf=False,
+            return_loo=True):
+        """One forward evaluation of the reference's per-iteration objective bodies
+        at theta.  Returns objectives {nlml, loo_crps, loo_logs, logdet, quad} and
+        the LOO predictive mean / variance (R&W eq. 5.12)."""
+        if X is not None:
+            self.set_data(X, y, kind=kind, Z=Z)
+        elif Z is not None:
+            self.set_inducing(Z)
+        if self.kind is None:
+            raise ValueError("no training data")
+        d = self._X.shape[1]
+        th, n_ell = pack_theta(theta, d)
+        obj = np.zeros(5)
+        n = self._X.shape[0]
+        mu = np.empty(n) if return_loo else None
+        var = np.empty(n) if return_loo else None
+        if self.kind == "full":
+            self.ctx.call("gps_full_fit", GPS_RBF if rbf else GPS_ARD, ptr(th), n_ell, ptr(obj),
+                          ptr(mu), ptr(var))
+        else:
+            if rbf:
+                raise ValueError("FITC uses the ARD kernel (K20:32-39)")
+            if self._Z is None:
+                raise ValueError("FITC needs inducing points Z")
+            self.ctx.call("gps_fitc_fit", ptr(th), n_ell, ptr(obj), ptr(mu), ptr(var))
+        return FitResult(self.kind, dict(zip(OBJ_NAMES, obj.tolist())), mu, var)
+
+    # --------------------------------------------------------------- predict
+    def predict(self, Xt=None, yt=None, with_scores=False):
+        """Predictive mean and variance (the diagonal of cal_mean_and_cov /
+        spgp_cal_mean_and_cov) at Xt with the last fit's factorisation."""
+        if Xt is not None:
+            self.set_test(Xt, yt)
+        nt = self._nt
+        mu, var, sc = np.empty(nt), np.empty(nt), np.zeros(6)
+        name = "gps_full_predict" if self.kind == "full" else "gps_fitc_predict"
+        self.ctx.call(name, ptr(mu), ptr(var), ptr(sc))
+        if with_scores:
+            return mu, var, dict(zip(SCORE_NAMES, sc.tolist()))
+        return mu, var
+
+    # ----------------------------------------------------------------- score
+    def score(self, mu, var, y_test, y_train):
+        """crps, logs, trivial_loss (MSLL), SMSE, MSE and ±2σ coverage (KF:276-292)."""
+        return score(mu, var, y_test, y_train, ctx=self.ctx)
+
+
+def score(mu, var, y_test, y_train, ctx=None):
+    ctx = ctx or _lib.default_context()
+    mu, var, yt = f64(mu).ravel(), f64(var).ravel(), f64(y_test).ravel()
+    ytr = f64(y_train).ravel()
+    out = np.zeros(6)
+    ctx.call("gps_scores", ptr(mu), ptr(var), ptr(yt), yt.size, float(ytr.mean()),
+             float(ytr.var(ddof=1)), ptr(out))
+    return dict(zip(SCORE_NAMES, out.tolist()))
+
+
+def fit(X, y, theta, kind="full", Z=None, rbf=False, ctx=None):
+    return GP(ctx).fit(X, y, theta, kind=kind, Z=Z, rbf=rbf)

@@ -1,0 +1,47 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (PKG_DIR, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")
+
+
+def golden_names(prefix=""):
+    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def theta_of(g):
+    """(log_sf2, log_ell, log_sn2, kind) of a golden case."""
+    if "theta" in g:
+        t = g["theta"]
+        return (float(t[0]), float(t[1]), float(t[2])), str(g.get("kern", "ARD"))
+    return (float(g["log_sf2"]), g["log_ell"], float(g["log_sn2"])), "ARD"
+
+
+def nrel(a, b):
+    """normwise relative error max|a-b| / max|b|."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import gpscore
+    return gpscore.Context(0)

@@ -1,0 +1,86 @@
+"""The CPU oracle (oracle/gp_oracle.py) pinned against the golden vectors that
+tests/golden/make_goldens.py produced by running the reference's own helper
+defs at fp64.  CPU only."""
+import numpy as np
+import pytest
+
+import gp_oracle as O
+from conftest import golden_names, load_golden, nrel, theta_of
+
+VEC_KEYS = ("loo_mu", "loo_var", "pred_mu", "pred_var")
+SCAL_KEYS = ("nlml", "loo_crps", "loo_logs", "logdet", "quad", "test_crps", "test_logs",
+             "test_msll", "test_smse", "test_mse", "test_cover")
+
+FULL = golden_names("sd_") + golden_names("full_")
+FITC = golden_names("fitc_")
+
+
+def _check(out, g, tol):
+    for k in VEC_KEYS:
+        assert nrel(out[k], g[k]) <= tol, (k, nrel(out[k], g[k]))
+    for k in SCAL_KEYS:
+        assert abs(out[k] - float(g[k])) <= tol * max(1.0, abs(float(g[k]))), (k, out[k], float(g[k]))
+
+
+@pytest.mark.parametrize("name", FULL)
+@pytest.mark.parametrize("flavour", ["ref", "fast"])
+def test_full_oracle_vs_golden(name, flavour):
+    g = load_golden(name)
+    th, kind = theta_of(g)
+    fn = O.ref_full if flavour == "ref" else O.fast_full
+    out = fn(g["X"], g["y"], g["Xt"], g["yt"], *th, kind="rbf" if kind == "rbf" else "ARD")
+    _check(out, g, 1e-9)
+
+
+@pytest.mark.parametrize("name", FITC)
+@pytest.mark.parametrize("flavour", ["ref", "fast", "shard3"])
+def test_fitc_oracle_vs_golden(name, flavour):
+    g = load_golden(name)
+    th, _ = theta_of(g)
+    if flavour == "ref":
+        out = O.ref_fitc(g["X"], g["y"], g["Xt"], g["yt"], g["Z"], *th)
+    else:
+        out = O.fast_fitc(g["X"], g["y"], g["Xt"], g["yt"], g["Z"], *th,
+                          shards=3 if flavour == "shard3" else 1)
+    _check(out, g, 1e-8)
+
+
+def test_l1_blocks():
+    g = load_golden("l1_blocks")
+    ell = g["log_ell"]
+    assert nrel(O.ref_ard(g["Xa"], g["Xb"], float(g["log_sf2"]), ell), g["ard_ab"]) < 1e-14
+    assert nrel(O.fast_gram(g["Xa"], g["Xb"], float(g["log_sf2"]), ell), g["ard_ab"]) < 1e-14
+    assert nrel(O.fast_gram(g["Xa"], g["Xb"], float(g["iso_log_sf2"]), float(g["iso_log_ell"])),
+                g["ard_iso"]) < 1e-14
+    assert nrel(O.fast_gram(g["x1"], g["x2"], float(g["rbf_log_sf2"]), float(g["rbf_log_ell2"]),
+                            kind="rbf"), g["rbf_12"]) < 1e-14
+    assert nrel(O.ref_chol_solve(g["B"], g["A"]), g["chol_solve"]) < 1e-12
+    assert nrel(O.fast_chol_solve(g["B"], g["A"]), g["chol_solve"]) < 1e-10
+    assert nrel(O.ref_chol_solve(np.eye(48), g["A"]), g["chol_solve_eye"]) < 1e-12
+    assert abs(O.ref_half_logdet(g["A"]) - float(g["half_logdet"])) < 1e-12
+    assert nrel(O.ref_Q(g["Xa"], g["nys_Z"], g["Xb"], float(g["log_sf2"]), ell), g["Q_ab"]) < 1e-10
+
+
+def test_scores():
+    g = load_golden("scores")
+    assert abs(O.crps(g["m"], g["c"], g["y"]) - float(g["crps"])) < 1e-14
+    assert abs(O.logs(g["m"], g["c"], g["y"]) - float(g["logs"])) < 1e-14
+    assert abs(O.trivial_loss(g["m"], g["c"], g["y"], g["y_train"]) - float(g["msll"])) < 1e-14
+    assert abs(O.smse(g["m"], g["y"], g["y_train"]) - float(g["smse"])) < 1e-14
+
+
+def test_loo_identity_bruteforce():
+    """LOO closed form (KF:241-244, R&W eq. 5.12) equals refitting without point i."""
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((40, 3))
+    y = rng.standard_normal(40)
+    th = (0.2, np.log([0.9, 1.3, 2.0]), np.log(0.05))
+    f = O.fast_full_fit(X, y, *th)
+    for i in (0, 17, 39):
+        keep = np.arange(40) != i
+        A = O.fast_gram(X[keep], X[keep], th[0], th[1], diag_add=np.exp(th[2]))
+        k = O.fast_gram(X[i:i + 1], X[keep], th[0], th[1]).ravel()
+        mu = k @ np.linalg.solve(A, y[keep])
+        var = np.exp(th[0]) + np.exp(th[2]) - k @ np.linalg.solve(A, k)
+        assert abs(mu - f["loo_mu"][i]) < 1e-12
+        assert abs(var - f["loo_var"][i]) < 1e-12
