@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""Benchmark of the GP hot path on MI355X (BASELINE.json metric).
+
+One step = one "unit" of the reference's per-iteration work at fixed theta:
+fit (Gram + Cholesky + L⁻¹ + α + diag(A⁻¹) → NLML, LOO-CRPS, LOO-LogS) + predict
+(μ*, σ²* at the test points) + score (CRPS, LogS, MSLL, SMSE, MSE, coverage).
+
+* Headline (``value``): full GP C3 (n = 20 000, d = 8, n* = 5 000), one unit per
+  rank per step.  The full GP does not shard (replicas only): under torchrun
+  every rank runs its own unit, value = units of all ranks / max-over-ranks time.
+* ``fitc``: FITC C5 (n = 200 000, m = 4 000, d = 16, n* = 10 000) with the rows
+  sharded over the ranks and ONE RCCL all-reduce of the m×m accumulator (strong
+  scaling: fixed total work); at N = 1 also C4 (n = 40 000, m = 2 000, d = 8).
+* ``roofline``: the FP64-MFMA GEMM kernel (potrf trailing updates, inverse,
+  predictive TRMM) — algorithmic flops / summed kernel time from hipEvents
+  recorded on the library's stream over the timed region; ``roofline_gram`` the
+  HBM-bound Gram kernel.
+* ``cpu_baseline``: the oracle's ref-mirror restatement of the reference op
+  sequence (oracle/gp_oracle.py, numpy/LAPACK, all threads) on a bounded C2-size
+  sample, extrapolated O(n³) to C3; rank 0 at N = 1 only.
+
+Inputs are synthetic (SURVEY.md §8d generator) and resident in HBM before the
+timed region.  Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd")
+sys.path.insert(0, PKG_DIR)
+
+METRIC = "GP fit+predict+CRPS wall-clock (ms) at n=20k full / n=40k FITC; HBM GB/s & MFMA%"
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, spec
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "C2": dict(n=5000, d=8, nt=1250, seed=2),
+    "C3": dict(n=20000, d=8, nt=5000, seed=3),
+    "C4": dict(n=40000, d=8, nt=10000, m=2000, seed=4),
+    "C5": dict(n=200000, d=16, nt=10000, m=4000, seed=5),
+}
+
+
+def synth(n, d, nt, seed, m=None):
+    """X, Xt ~ N(0, I); y = sin(3 X w) + 0.1 ε; Z = m training rows."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, d))
+    Xt = rng.standard_normal((nt, d))
+    w = rng.standard_normal(d) / np.sqrt(d)
+    y = np.sin(3 * X @ w) + 0.1 * rng.standard_normal(n)
+    yt = np.sin(3 * Xt @ w) + 0.1 * rng.standard_normal(nt)
+    Z = X[rng.choice(n, m, replace=False)] if m else None
+    theta = (0.0, np.log(2.0) * np.ones(d), np.log(0.01))
+    return X, y, Xt, yt, Z, theta
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+class Ctl:
+    """Control plane: barrier and max-over-ranks (gloo on the host; the data-path
+    collective is RCCL inside libgpscore)."""
+
+    def __init__(self, world):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v):
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+
+def sync_all(ctl, ctx):
+    ctx.synchronize()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+    ctl.barrier()
+
+
+def timed(ctl, ctx, fn, steps):
+    sync_all(ctl, ctx)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync_all(ctl, ctx)
+    return ctl.max(time.perf_counter() - t0)
+
+
+def kernel_summary(prof, steps):
+    """per-step kernel stats from the library's hipEvent records."""
+    out = {}
+    for tag, v in sorted(prof.items()):
+        out[tag] = {"count": v["count"] / steps, "ms": v["ms"] / steps,
+                    "tflops": (v["flop"] / (v["ms"] * 1e-3) / 1e12) if v["flop"] and v["ms"] else None,
+                    "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["bytes"] and v["ms"] else None}
+    return out
+
+
+def roofline_mfma(prof, traffic=None):
+    f = sum(v["flop"] for k, v in prof.items() if k.startswith("gemm"))
+    ms = sum(v["ms"] for k, v in prof.items() if k.startswith("gemm"))
+    n = sum(v["count"] for k, v in prof.items() if k.startswith("gemm"))
+    ach = f / (ms * 1e-3) / 1e12 if ms else 0.0
+    return {"bound": "mfma", "kernel": "gemm_f64_kernel (all launches of the step)",
+            "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
+            "launches_per_step": n, "avg_launch_ms": ms / n if n else None,
+            "flop_per_launch": f / n if n else None}
+
+
+def roofline_gram(prof, tags=("gram_kff", "gram_ksf")):
+    b = sum(prof[t]["bytes"] for t in tags if t in prof)
+    ms = sum(prof[t]["ms"] for t in tags if t in prof)
+    ach = b / (ms * 1e-3) / 1e9 if ms else 0.0
+    return {"bound": "hbm", "kernel": "gram_kernel<8> (K_ff lower + K*f)", "achieved": round(ach, 1),
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+            "traffic": None, "bytes_per_step": b}
+
+
+def cpu_baseline():
+    """ref-mirror oracle (reference op sequence) on C2, extrapolated to C3."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import gp_oracle as O
+    c = CONFIGS["C2"]
+    X, y, Xt, yt, _, th = synth(c["n"], c["d"], c["nt"], c["seed"])
+    t0 = time.perf_counter()
+    O.ref_full(X, y, Xt, yt, *th)
+    t = time.perf_counter() - t0
+    scale = (CONFIGS["C3"]["n"] / c["n"]) ** 3
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": 1.0 / (t * scale), "unit": "fit+predict+score units/s (C3, extrapolated)",
+            "cores": cores, "kind": "port",
+            "sample": f"oracle ref_full (reference op sequence: upper potrf + 2 LU solves per "
+                      f"chol_solve, full n*×n* cov) on C2 n={c['n']} d={c['d']} n*={c['nt']}: "
+                      f"{t:.2f} s, ×{scale:.0f} (O(n³), n and n* both ×4) → C3 "
+                      f"{t * scale:.1f} s/unit"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--no-fitc", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    ctl = Ctl(world)
+    import gpscore
+    ctx = gpscore.Context(local)
+    gp = gpscore.GP(ctx=ctx)
+
+    # ---------------- full GP (replicas) ----------------
+    c = CONFIGS[args.config]
+    X, y, Xt, yt, _, th = synth(c["n"], c["d"], c["nt"], c["seed"])
+    gp.set_data(X, y)
+    gp.set_test(Xt, yt)
+
+    def unit():
+        gp.fit(theta=th, return_loo=False)
+        return gp.predict(with_scores=True)
+
+    for _ in range(args.warmup):
+        unit()
+    ctx.prof(True)
+    t_full = timed(ctl, ctx, unit, args.steps)
+    prof = ctx.prof_collect()
+    ctx.prof(False)
+    ms_full = 1e3 * t_full / args.steps
+    obj = gp.fit(theta=th, return_loo=False).objectives
+    _, _, sc = gp.predict(with_scores=True)
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("gemm_per_launch_bytes")
+        except Exception:
+            traffic = None
+
+    res = {
+        "metric": METRIC,
+        "value": world * args.steps / t_full,
+        "unit": f"fit+predict+score units/s ({args.config} full GP, whole job)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_full,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (SURVEY.md §8d generator; random-init theta fixed)",
+        "config": {"workload": f"{args.config} full GP fit(NLML+LOO-CRPS+LOO-LogS)+predict+score",
+                   "n": c["n"], "d": c["d"], "n_test": c["nt"], "kernel": "ARD",
+                   "parallelism": "replicas" if world > 1 else "single"},
+        "roofline": roofline_mfma(prof, traffic),
+        "roofline_gram": roofline_gram(prof),
+        "objectives": obj, "scores": sc,
+        "kernels_per_step": kernel_summary(prof, args.steps),
+    }
+
+    # ---------------- FITC (rows sharded, RCCL all-reduce) ----------------
+    if not args.no_fitc:
+        from gpscore.dist import shard_rows
+        fitc = {}
+        legs = ["C5"] + (["C4"] if world == 1 else [])
+        fgp = gpscore.GP(ctx=ctx)
+        if world > 1:
+            import ctypes
+            lib = gpscore.load()
+            uid = None
+            if rank == 0:
+                buf = ctypes.create_string_buffer(128)
+                ctx.check(lib.gps_comm_unique_id(buf), "gps_comm_unique_id")
+                uid = buf.raw
+            obj_l = [uid]
+            ctl.dist.broadcast_object_list(obj_l, src=0)
+            ctx.call("gps_comm_init", world, rank, ctypes.create_string_buffer(obj_l[0], 128))
+        for leg in legs:
+            fc = CONFIGS[leg]
+            Xf, yf, Xtf, ytf, Z, thf = synth(fc["n"], fc["d"], fc["nt"], fc["seed"], fc["m"])
+            a, b = shard_rows(fc["n"], world, rank)
+            ta, tb = shard_rows(fc["nt"], world, rank)
+            fgp.set_data(Xf[a:b], yf[a:b], kind="fitc", Z=Z, n_total=fc["n"],
+                         ytr_stats=(float(yf.mean()), float(yf.var(ddof=1))))
+            fgp.set_test(Xtf[ta:tb], ytf[ta:tb], nt_total=fc["nt"])
+
+            def funit():
+                fgp.fit(theta=thf, return_loo=False)
+                return fgp.predict(with_scores=True)
+
+            for _ in range(args.warmup):
+                funit()
+            ctx.prof(True)
+            tf = timed(ctl, ctx, funit, args.steps)
+            fprof = ctx.prof_collect()
+            ctx.prof(False)
+            fobj = fgp.fit(theta=thf, return_loo=False).objectives
+            fitc[leg] = {"ms_per_step": 1e3 * tf / args.steps,
+                         "units_per_s": args.steps / tf,
+                         "config": {"n": fc["n"], "m": fc["m"], "d": fc["d"], "n_test": fc["nt"],
+                                    "rows_per_rank": b - a, "ranks": world},
+                         "scaling": "strong",
+                         "objectives": fobj,
+                         "roofline": roofline_mfma(fprof),
+                         "kernels_per_step": kernel_summary(fprof, args.steps)}
+            del Xf, yf, Xtf, ytf
+        if world > 1:
+            ctx.call("gps_comm_destroy")
+        res["fitc"] = fitc
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline()
+        res["cpu_baseline"] = cb
+        res["speedup_vs_cpu"] = res["value"] / cb["value"]
+    if rank == 0:
+        print(json.dumps(res))
+    if ctl.dist:
+        ctl.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

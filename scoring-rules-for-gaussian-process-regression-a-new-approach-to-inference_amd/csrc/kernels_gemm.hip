@@ -34,6 +34,12 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int BM = 128, BN = 128, BK = 16, LS = 144;
 constexpr int STAGE = 2 * BK * LS;  // doubles per buffer (A image + B image)
 
+constexpr int GROUP_M = 8;
+
+// logical tile id -> (ti, tj).  Lower-triangular enumeration for SYRK outputs;
+// otherwise a grouped raster (GROUP_M tile rows at a time, column-major inside
+// the group) so the tiles resident together share A and B panels in L2.  For
+// triangular operands the tiles with the longest K range are issued first.
 __device__ __forceinline__ void tile_of(const GemmParams& p, int t, int& ti, int& tj) {
   if (p.lower_out) {
     int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -41,10 +47,17 @@ __device__ __forceinline__ void tile_of(const GemmParams& p, int t, int& ti, int
     while (r * (r + 1) / 2 > t) --r;
     ti = r;
     tj = t - r * (r + 1) / 2;
-  } else {
-    ti = t / p.tiles_n;
-    tj = t - ti * p.tiles_n;
+    return;
   }
+  const int per_group = GROUP_M * p.tiles_n;
+  const int g = t / per_group;
+  const int first = g * GROUP_M;
+  const int gm = min(GROUP_M, p.tiles_m - first);
+  const int tt = t - g * per_group;
+  ti = first + tt % gm;
+  tj = tt / gm;
+  if (p.tri == TRI_K_LE_I) ti = p.tiles_m - 1 - ti;
+  else if (p.tri == TRI_K_LE_J) tj = p.tiles_n - 1 - tj;
 }
 
 // bijective XCD-contiguous remap: blocks b, b+8, b+16, ... (one XCD under the
@@ -154,32 +167,38 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
 
+  auto compute = [&](int buf) {
+    const double* As = smem + buf * STAGE;
+    const double* Bs = As + BK * LS;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      const int krow = (kk * 4 + (lane >> 4)) * LS + (lane & 15);
+      double a[4], b[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = As[krow + wr * 64 + mi * 16];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) b[ni] = Bs[krow + wc * 64 + ni * 16];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+    }
+  };
+
   if (nk > 0) {
     load_tile(kb);
     store_tile(0);
     __syncthreads();
-    for (int it = 0; it < nk; ++it) {
-      const int cur = it & 1;
-      if (it + 1 < nk) load_tile(kb + (it + 1) * BK);
-      const double* As = smem + cur * STAGE;
-      const double* Bs = As + BK * LS;
-#pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
-        const int krow = (kk * 4 + (lane >> 4)) * LS + (lane & 15);
-        double a[4], b[4];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) a[mi] = As[krow + wr * 64 + mi * 16];
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b[ni] = Bs[krow + wc * 64 + ni * 16];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-      }
-      if (it + 1 < nk) store_tile(cur ^ 1);
+    // steady state: prefetch slice it+1 into registers, multiply slice it, then
+    // park the prefetched slice in the other LDS buffer (no branches in the body)
+    for (int it = 0; it < nk - 1; ++it) {
+      load_tile(kb + (it + 1) * BK);
+      compute(it & 1);
+      store_tile((it + 1) & 1);
       __syncthreads();
     }
+    compute((nk - 1) & 1);
   }
 
   const int lrow = lane >> 4, lcol = lane & 15;

@@ -1,90 +1,221 @@
 // Diagonal-block kernel of the blocked Cholesky (replaces LAPACK ?potrf behind
-// torch.potrf, KF:26 / KF:332).  One 1024-thread workgroup holds a whole
-// 128×128 fp64 block in LDS (136 KiB of the CU's 160 KiB) and
-//   1. factors it A = L Lᵀ (right-looking, one barrier per column; the
-//      column is kept unscaled during the sweep and scaled once at the end),
-//   2. records log L_ii (the ½log|A| terms of KF:332) and the first
-//      non-positive pivot (torch.potrf's "leading minor not PD" error),
-//   3. inverts L in place (LAPACK trti2 order: columns right to left,
-//      x = -L_jj⁻¹ · L⁻¹[j+1:, j+1:] · L[j+1:, j]),
-//   4. writes L⁻¹ with explicit zeros above the diagonal.
-// Thread layout: 8 consecutive lanes own one row (16 waves × 8 rows); a row's
-// partial dot products are combined with in-wave xor shuffles.  LDS row stride
-// 136 doubles (≡ 16 dwords mod 64) keeps the 4-row × 8-column lane footprint of
-// a ds_read_b64 conflict-free.
+// torch.potrf, KF:26 / KF:332) fused with the block's triangular inverse.
+//
+// One 1024-thread workgroup owns a 128×128 fp64 block.  Thread t holds the 4×4
+// sub-block (br, bc) = (t >> 5, t & 31) in registers; only the 528 lower
+// sub-blocks do arithmetic.  The block is processed in 32 panel steps of width 4:
+//
+//   factor, step jb (two barriers):
+//     1. thread (jb, jb) factors its 4×4 diagonal block in registers, inverts
+//        it (D⁻¹), records log L_ii (the ½log|A| terms of KF:332) and the first
+//        non-positive pivot (torch.potrf's "leading minor not PD"), and
+//        publishes L_jj and D⁻¹ to LDS;
+//     2. the panel threads (br > jb, bc = jb) form L_rb = A_rb D⁻ᵀ and publish it;
+//     3. every trailing thread (br >= bc > jb) applies the rank-4 update
+//        A_rc -= L_rb L_cbᵀ from LDS.  The diagonal thread of step jb+1 finishes
+//        its own update first and factors immediately (natural look-ahead).
+//   invert, step ib (one barrier): X = L⁻¹ by block forward substitution on
+//     X = I held in the same registers: block row ib is finalised
+//     X_ib ← D_ib⁻¹ X_ib and published, then every block row r > ib does
+//     X_r -= L_r,ib X_ib.
+// L is kept transposed in LDS (LT[col][row], 132-double rows) so a thread's
+// 4-row slice of an L column is one contiguous 32-byte read.
 #include "gps_internal.h"
 
 namespace gps {
 
 constexpr int NB = 128;
-constexpr int SL = 136;
+constexpr int LTS = 132;
+
+__device__ __forceinline__ void lds_read4(const double* p, double (&v)[4]) {
+  const double2 a = *reinterpret_cast<const double2*>(p);
+  const double2 b = *reinterpret_cast<const double2*>(p + 2);
+  v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
 
 __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restrict__ A, int64_t lda,
                                                           double* __restrict__ Linv, int64_t ldl,
                                                           double* __restrict__ Lout, int64_t ldlo,
                                                           double* __restrict__ logdiag, int* info,
                                                           int base, int nreal) {
-  __shared__ __attribute__((aligned(16))) double a[NB * SL];
-  __shared__ double sq[NB];
+  __shared__ __attribute__((aligned(16))) double LT[NB * LTS];   // LT[col][row] = L[row][col]
+  __shared__ __attribute__((aligned(16))) double DI[32 * 16];    // D_b⁻¹ (4×4, row-major) per block
+  __shared__ __attribute__((aligned(16))) double XB[2 * 4 * NB]; // published X block row [4][128]
   const int tid = threadIdx.x;
-  for (int e = tid; e < NB * NB / 2; e += 1024) {
-    const int r = e >> 6, c = (e & 63) * 2;
-    const double2 v = *reinterpret_cast<const double2*>(A + (int64_t)r * lda + c);
-    *reinterpret_cast<double2*>(&a[r * SL + c]) = v;
+  const int br = tid >> 5, bc = tid & 31;
+  const bool lower = bc <= br;
+  const int r0 = br * 4, c0 = bc * 4;
+
+  double a[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (lower) {
+      const double2* src = reinterpret_cast<const double2*>(A + (int64_t)(r0 + r) * lda + c0);
+      const double2 u = src[0], v = src[1];
+      a[r][0] = u.x; a[r][1] = u.y; a[r][2] = v.x; a[r][3] = v.y;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a[r][c] = 0.0;
+    }
+  }
+
+  // ======================= factorisation =======================
+  for (int jb = 0; jb < 32; ++jb) {
+    if (br == jb && bc == jb) {
+      // 4×4 Cholesky in registers
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double d = a[j][j];
+        if (!(d > 0.0) && 4 * jb + j < nreal) atomicMin(info, base + 4 * jb + j + 1);
+        const double s = sqrt(d), is = 1.0 / s;
+        a[j][j] = s;
+        logdiag[4 * jb + j] = log(s);
+#pragma unroll
+        for (int r = j + 1; r < 4; ++r) a[r][j] *= is;
+#pragma unroll
+        for (int r = j + 1; r < 4; ++r)
+#pragma unroll
+          for (int c = j + 1; c <= r; ++c) a[r][c] = fma(-a[r][j], a[c][j], a[r][c]);
+      }
+      // D⁻¹ by forward substitution
+      double x[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double s = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+          for (int k = 0; k < r; ++k) s = fma(-a[r][k], x[k][c], s);
+          x[r][c] = (r >= c) ? s / a[r][r] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          DI[jb * 16 + r * 4 + c] = x[r][c];
+          LT[(c0 + c) * LTS + r0 + r] = (c <= r) ? a[r][c] : 0.0;
+        }
+    }
+    __syncthreads();
+    if (lower && bc == jb && br > jb) {  // panel: L_rb = A_rb D⁻ᵀ
+      double di[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lds_read4(&DI[jb * 16 + r * 4], di[r]);
+      double l[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k <= c; ++k) s = fma(a[r][k], di[c][k], s);
+          l[r][c] = s;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          a[r][c] = l[r][c];
+          LT[(c0 + c) * LTS + r0 + r] = l[r][c];
+        }
+    }
+    __syncthreads();
+    if (lower && bc > jb) {  // trailing rank-4 update
+      double lr[4][4], lc[4][4];  // [k][r]
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lds_read4(&LT[(4 * jb + k) * LTS + r0], lr[k]);
+        lds_read4(&LT[(4 * jb + k) * LTS + c0], lc[k]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double s = a[r][c];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s = fma(-lr[k][r], lc[k][c], s);
+          a[r][c] = s;
+        }
+    }
   }
   __syncthreads();
 
-  const int i = tid >> 3, c = tid & 7;
-  // ---- 1. unscaled right-looking factorisation: a[i][k] -= a[i][j] a[k][j] / d_j
-  for (int j = 0; j < NB - 1; ++j) {
-    if (i > j) {
-      const double f = a[i * SL + j] / a[j * SL + j];
-      for (int k = j + 1 + c; k <= i; k += 8) a[i * SL + k] = fma(-f, a[k * SL + j], a[i * SL + k]);
-    }
-    __syncthreads();
-  }
-  // ---- 2. pivots, log-diagonal, PD check
-  if (tid < NB) {
-    const double dj = a[tid * SL + tid];
-    if (!(dj > 0.0) && tid < nreal) atomicMin(info, base + tid + 1);
-    const double sj = sqrt(dj);
-    sq[tid] = sj;
-    logdiag[tid] = log(sj);
-  }
-  __syncthreads();
-  for (int k = c; k <= i; k += 8) a[i * SL + k] /= sq[k];
-  __syncthreads();
   if (Lout) {
-    for (int e = tid; e < NB * NB; e += 1024) {
-      const int r = e >> 7, cc = e & 127;
-      Lout[(int64_t)r * ldlo + cc] = cc <= r ? a[r * SL + cc] : 0.0;
+    for (int e = tid; e < NB * NB / 2; e += 1024) {
+      const int r = e >> 6, c = (e & 63) * 2;
+      const double v0 = c <= r ? LT[c * LTS + r] : 0.0;
+      const double v1 = c + 1 <= r ? LT[(c + 1) * LTS + r] : 0.0;
+      *reinterpret_cast<double2*>(Lout + (int64_t)r * ldlo + c) = make_double2(v0, v1);
     }
   }
-  // ---- 3. in-place inverse, columns right to left
-  for (int j = NB - 1; j >= 0; --j) {
-    double s = 0.0;
-    if (i > j)
-      for (int k = j + 1 + c; k <= i; k += 8) s = fma(a[i * SL + k], a[k * SL + j], s);
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
-    const double ljj = a[j * SL + j];
+
+  // ======================= X = L⁻¹ =======================
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[r][c] = (r0 + r == c0 + c) ? 1.0 : 0.0;
+
+  for (int ib = 0; ib < 32; ++ib) {
+    double* xb = XB + (ib & 1) * 4 * NB;
+    if (lower && br == ib) {  // X_ib ← D_ib⁻¹ X_ib, publish
+      double di[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lds_read4(&DI[ib * 16 + r * 4], di[r]);
+      double x[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k <= r; ++k) s = fma(di[r][k], a[k][c], s);
+          x[r][c] = s;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[r][c] = x[r][c];
+        *reinterpret_cast<double2*>(&xb[r * NB + c0]) = make_double2(x[r][0], x[r][1]);
+        *reinterpret_cast<double2*>(&xb[r * NB + c0 + 2]) = make_double2(x[r][2], x[r][3]);
+      }
+    }
     __syncthreads();
-    if (i > j && c == 0) a[i * SL + j] = -s / ljj;
-    if (tid == 0) a[j * SL + j] = 1.0 / ljj;
-    __syncthreads();
+    if (lower && br > ib && bc <= ib) {  // X_r -= L_r,ib X_ib
+      double lr[4][4], xi[4][4];  // lr[k][r] = L[r0+r][4ib+k]; xi[k][c] = X[4ib+k][c0+c]
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lds_read4(&LT[(4 * ib + k) * LTS + r0], lr[k]);
+        lds_read4(&xb[k * NB + c0], xi[k]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double s = a[r][c];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s = fma(-lr[k][r], xi[k][c], s);
+          a[r][c] = s;
+        }
+    }
   }
-  // ---- 4. write L⁻¹ (lower, explicit zeros above the diagonal)
-  for (int e = tid; e < NB * NB; e += 1024) {
-    const int r = e >> 7, cc = e & 127;
-    Linv[(int64_t)r * ldl + cc] = cc <= r ? a[r * SL + cc] : 0.0;
+
+  // write L⁻¹ (explicit zeros above the diagonal)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = (lower && c0 + c <= r0 + r) ? a[r][c] : 0.0;
+    double2* dst = reinterpret_cast<double2*>(Linv + (int64_t)(r0 + r) * ldl + c0);
+    dst[0] = make_double2(v[0], v[1]);
+    dst[1] = make_double2(v[2], v[3]);
   }
 }
 
 hipError_t launch_potrf_diag(const double* A, int64_t lda, double* Linv, int64_t ldl, double* Lout,
                              int64_t ldlo, double* logdiag, int* info, int base, int nreal,
                              hipStream_t s) {
-  if ((lda & 1) || (ldl & 1)) return hipErrorInvalidValue;
+  if ((lda & 1) || (ldl & 1) || (Lout && (ldlo & 1))) return hipErrorInvalidValue;
   hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(1024), 0, s, A, lda, Linv, ldl, Lout, ldlo,
                      logdiag, info, base, nreal);
   return hipGetLastError();
