@@ -180,13 +180,19 @@ GemmParams gp0() {
   return p;
 }
 
+// profiling tag: operation + size class (s: < 16 output tiles, m: < 256, l: >= 256)
 const char* gemm_tag(int al, int bl, int epi, const GemmParams& p) {
-  if (epi == EPI_COLRED) return "gemm_trmm_colred";
-  if (epi == EPI_ROWSQ) return "gemm_rowsq";
-  if (p.lower_out) return p.ksplit > 1 ? "gemm_syrk_splitk" : "gemm_syrk";
   (void)al;
   (void)bl;
-  return p.tri ? "gemm_trmm" : "gemm";
+  if (epi == EPI_COLRED) return "gemm_trmm_colred";
+  if (epi == EPI_ROWSQ) return "gemm_rowsq";
+  const int64_t tiles = (int64_t)(p.M / GPS_TILE) * (p.N / GPS_TILE) / (p.lower_out ? 2 : 1);
+  const int cls = tiles < 16 ? 0 : (tiles < 256 ? 1 : 2);
+  static const char* syrk[3] = {"gemm_syrk_s", "gemm_syrk_m", "gemm_syrk_l"};
+  static const char* trmm[3] = {"gemm_trmm_s", "gemm_trmm_m", "gemm_trmm_l"};
+  static const char* plain[3] = {"gemm_s", "gemm_m", "gemm_l"};
+  if (p.lower_out) return p.ksplit > 1 ? "gemm_syrk_splitk" : syrk[cls];
+  return p.tri ? trmm[cls] : plain[cls];
 }
 
 // algorithmic flops of one launch (triangular operands counted at their nonzero half)

@@ -57,6 +57,7 @@ struct GemmParams {
   int ksplit;                // number of K slices (grid.y)
   int tri;
   int tiles_m, tiles_n;
+  int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap
 };
 
 // ------------------------------------------------------------------ launchers

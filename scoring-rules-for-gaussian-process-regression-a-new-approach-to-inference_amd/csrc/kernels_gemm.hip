@@ -9,37 +9,48 @@
 // (reference: chol_solve KF:25-29, half-logdet KF:332, cal_mean_and_cov KF:121-126,
 //  Q KF:32-39, spgp_cal_mean_and_cov K20:76-83 — all LAPACK/BLAS on the CPU there).
 //
-// Geometry: 128×128 output tile per 256-thread workgroup (4 waves, each a 64×64
-// sub-tile = 4×4 blocks of v_mfma_f64_16x16x4_f64), K staged through LDS in
-// 16-deep slices, double-buffered (global→register prefetch of slice k+1 while
-// slice k is multiplied).  LDS images are k-major [k][128 + 16]: a fragment read
-// (16 consecutive doubles per k row, 4 k rows per wave instruction) then hits
-// all 64 banks without conflict (row stride ≡ 32 dwords mod 64).
+// Geometry: a TILE×TILE output tile per 256-thread workgroup (TILE = 128 for
+// large grids, 64 for the latency-bound small grids at the bottom of the
+// recursion); 4 waves, each a (TILE/2)² sub-tile of v_mfma_f64_16x16x4_f64
+// blocks.  K is staged through LDS in 16-deep slices, double-buffered
+// (global→register prefetch of slice k+1 while slice k is multiplied).  LDS
+// images are k-major [k][TILE + 16]: a fragment read (16 consecutive doubles per
+// k row, 4 k rows per wave instruction) hits all 64 banks without conflict (row
+// stride ≡ 32 dwords mod 64).
 //
-// f64 MFMA operand map (cdna_hip_programming.md §3): lane l supplies
-// A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; accumulator register r of
-// lane l is C[row = (l>>4) + 4r][col = l&15].
+// f64 MFMA operand map (cdna_hip_programming.md §3; checked on the box by
+// tools/mfma_f64_probe.hip): lane l supplies A[i = l&15][k = l>>4] and
+// B[k = l>>4][j = l&15]; accumulator register r of lane l is
+// C[row = (l>>4) + 4r][col = l&15].  Built with -mllvm -amdgpu-mfma-vgpr-form=1:
+// without it hipcc keeps the accumulators in VGPRs and copies them to AGPRs and
+// back around every MFMA chain (measured: 35 TF/s instead of 77 on a pure MFMA
+// loop, tools/mfma_f64_sweep.hip).
 //
-// Triangular operands are handled by clipping the K range per output tile at
-// 128-granularity (the diagonal tiles of a triangular factor are stored with
-// explicit zeros above the diagonal), so no multiply touches a tile that is
-// structurally zero.  Workgroup ids are remapped so that the tiles one XCD
-// runs are contiguous in tile order (shared A rows stay in that XCD's L2).
+// Triangular operands are handled by clipping the K range per output tile (the
+// diagonal 128-blocks of a triangular factor are stored with explicit zeros
+// above the diagonal, so clipping at 64 or 128 granularity never drops a
+// nonzero) — no multiply touches a structurally zero tile.
 #include "gps_internal.h"
 
 namespace gps {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128, BN = 128, BK = 16, LS = 144;
-constexpr int STAGE = 2 * BK * LS;  // doubles per buffer (A image + B image)
-
+constexpr int BK = 16;
 constexpr int GROUP_M = 8;
 
-// logical tile id -> (ti, tj).  Lower-triangular enumeration for SYRK outputs;
-// otherwise a grouped raster (GROUP_M tile rows at a time, column-major inside
-// the group) so the tiles resident together share A and B panels in L2.  For
-// triangular operands the tiles with the longest K range are issued first.
+// logical tile id -> (ti, tj).  Lower-triangular enumeration for SYRK outputs
+// (uniform work per tile); otherwise a grouped raster (GROUP_M tile rows at a
+// time, column-major inside the group) so the tiles resident together share A
+// and B panels in L2.
+//
+// Triangular operands (work per tile grows linearly along one tile index) are
+// issued heaviest-first and WITHOUT the XCD-contiguous remap.  Measured on
+// MI355X (tools/gemm_bench.cpp, 20096×5120×20096 TRMM): remap + any order
+// 35-45 TF/s, plain grouped order 64.6, heaviest-first 68.9.  Workgroups are
+// dealt to XCDs in block order, so an XCD whose slots are all held by long tiles
+// stalls the dispatch of every later block; equal-work neighbours in block order
+// (which land on different XCDs) avoid that.
 __device__ __forceinline__ void tile_of(const GemmParams& p, int t, int& ti, int& tj) {
   if (p.lower_out) {
     int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
@@ -56,8 +67,10 @@ __device__ __forceinline__ void tile_of(const GemmParams& p, int t, int& ti, int
   const int tt = t - g * per_group;
   ti = first + tt % gm;
   tj = tt / gm;
-  if (p.tri == TRI_K_LE_I) ti = p.tiles_m - 1 - ti;
-  else if (p.tri == TRI_K_LE_J) tj = p.tiles_n - 1 - tj;
+  if (p.map_mode != 0) return;
+  if (p.tri == TRI_K_LE_I) ti = p.tiles_m - 1 - ti;       // K grows with ti
+  else if (p.tri == TRI_K_LE_J) tj = p.tiles_n - 1 - tj;  // K grows with tj
+  // TRI_K_GE_I / TRI_K_GE_J: K shrinks with the index, natural order is heaviest-first
 }
 
 // bijective XCD-contiguous remap: blocks b, b+8, b+16, ... (one XCD under the
@@ -67,20 +80,29 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <int ALAY, int BLAY, int EPI>
+template <int ALAY, int BLAY, int EPI, int TILE>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
+  constexpr int LS = TILE + 16;          // LDS row stride (doubles)
+  constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
+  constexpr int WT = TILE / 2;           // per-wave sub-tile edge
+  constexpr int MI = WT / 16;            // MFMA blocks per wave edge
+  constexpr int PER = TILE * BK / 256;   // doubles of one operand slice per thread (8 or 4)
+  constexpr int NQ = PER / 2;            // 16-byte loads per operand per thread
+  constexpr int TPR = TILE / PER;        // threads per k-row for k-major sources
+  constexpr int TPI = BK / PER;          // threads per i-row for i-major sources
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
 
   int ti, tj;
-  tile_of(p, xcd_remap(blockIdx.x, gridDim.x), ti, tj);
-  const int row0 = ti * BM, col0 = tj * BN;
+  const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
+  tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj);
+  const int row0 = ti * TILE, col0 = tj * TILE;
 
   int kb = 0, ke = p.K;
   switch (p.tri) {
-    case TRI_K_LE_I: ke = min(ke, row0 + BM); break;
-    case TRI_K_LE_J: ke = min(ke, col0 + BN); break;
+    case TRI_K_LE_I: ke = min(ke, row0 + TILE); break;
+    case TRI_K_LE_J: ke = min(ke, col0 + TILE); break;
     case TRI_K_GE_J: kb = col0; break;
     case TRI_K_GE_I: kb = row0; break;
     default: break;
@@ -94,78 +116,78 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   }
   const int nk = ke > kb ? (ke - kb) / BK : 0;
 
-  // ---- global -> register staging (8 doubles of A and 8 of B per thread) ----
-  double2 ra[4], rb[4];
+  // ---- global -> register staging (PER doubles of A and of B per thread) ----
+  double2 ra[NQ], rb[NQ];
   auto load_tile = [&](int k0) {
     if constexpr (ALAY == LAY_T) {  // A stored [k][i]
-      const int k = tid >> 4, i = (tid & 15) * 8;
+      const int k = tid / TPR, i = (tid % TPR) * PER;
       const double2* src = reinterpret_cast<const double2*>(p.A + (int64_t)(k0 + k) * p.lda + row0 + i);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = src[q];
+      for (int q = 0; q < NQ; ++q) ra[q] = src[q];
       if (p.kscale) {
         const double sc = p.kscale[k0 + k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { ra[q].x *= sc; ra[q].y *= sc; }
+        for (int q = 0; q < NQ; ++q) { ra[q].x *= sc; ra[q].y *= sc; }
       }
     } else {  // A stored [i][k]
-      const int i = tid >> 1, k = (tid & 1) * 8;
+      const int i = tid / TPI, k = (tid % TPI) * PER;
       const double2* src = reinterpret_cast<const double2*>(p.A + (int64_t)(row0 + i) * p.lda + k0 + k);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = src[q];
+      for (int q = 0; q < NQ; ++q) ra[q] = src[q];
       if (p.kscale) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           ra[q].x *= p.kscale[k0 + k + 2 * q];
           ra[q].y *= p.kscale[k0 + k + 2 * q + 1];
         }
       }
     }
     if constexpr (BLAY == LAY_N) {  // B stored [k][j]
-      const int k = tid >> 4, j = (tid & 15) * 8;
+      const int k = tid / TPR, j = (tid % TPR) * PER;
       const double2* src = reinterpret_cast<const double2*>(p.B + (int64_t)(k0 + k) * p.ldb + col0 + j);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rb[q] = src[q];
+      for (int q = 0; q < NQ; ++q) rb[q] = src[q];
     } else {  // B stored [j][k]
-      const int j = tid >> 1, k = (tid & 1) * 8;
+      const int j = tid / TPI, k = (tid % TPI) * PER;
       const double2* src = reinterpret_cast<const double2*>(p.B + (int64_t)(col0 + j) * p.ldb + k0 + k);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rb[q] = src[q];
+      for (int q = 0; q < NQ; ++q) rb[q] = src[q];
     }
   };
   auto store_tile = [&](int buf) {
     double* As = smem + buf * STAGE;
     double* Bs = As + BK * LS;
     if constexpr (ALAY == LAY_T) {
-      const int k = tid >> 4, i = (tid & 15) * 8;
+      const int k = tid / TPR, i = (tid % TPR) * PER;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(&As[k * LS + i + 2 * q]) = ra[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&As[k * LS + i + 2 * q]) = ra[q];
     } else {
-      const int i = tid >> 1, k = (tid & 1) * 8;
+      const int i = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         As[(k + 2 * q) * LS + i] = ra[q].x;
         As[(k + 2 * q + 1) * LS + i] = ra[q].y;
       }
     }
     if constexpr (BLAY == LAY_N) {
-      const int k = tid >> 4, j = (tid & 15) * 8;
+      const int k = tid / TPR, j = (tid % TPR) * PER;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(&Bs[k * LS + j + 2 * q]) = rb[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&Bs[k * LS + j + 2 * q]) = rb[q];
     } else {
-      const int j = tid >> 1, k = (tid & 1) * 8;
+      const int j = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         Bs[(k + 2 * q) * LS + j] = rb[q].x;
         Bs[(k + 2 * q + 1) * LS + j] = rb[q].y;
       }
     }
   };
 
-  d4 acc[4][4];
+  d4 acc[MI][MI];
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
+    for (int ni = 0; ni < MI; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
 
   auto compute = [&](int buf) {
     const double* As = smem + buf * STAGE;
@@ -173,15 +195,15 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
       const int krow = (kk * 4 + (lane >> 4)) * LS + (lane & 15);
-      double a[4], b[4];
+      double a[MI], b[MI];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = As[krow + wr * 64 + mi * 16];
+      for (int mi = 0; mi < MI; ++mi) a[mi] = As[krow + wr * WT + mi * 16];
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) b[ni] = Bs[krow + wc * 64 + ni * 16];
+      for (int ni = 0; ni < MI; ++ni) b[ni] = Bs[krow + wc * WT + ni * 16];
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < MI; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
     }
   };
@@ -205,51 +227,51 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   if constexpr (EPI == EPI_STORE) {
     double* Cb = p.C + (int64_t)blockIdx.y * p.c_kslice_stride;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = row0 + wr * 64 + mi * 16 + lrow + 4 * r;
-        double* crow = Cb + (int64_t)row * p.ldc + col0 + wc * 64 + lcol;
+        const int row = row0 + wr * WT + mi * 16 + lrow + 4 * r;
+        double* crow = Cb + (int64_t)row * p.ldc + col0 + wc * WT + lcol;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
+        for (int ni = 0; ni < MI; ++ni) {
           double v = p.alpha * acc[mi][ni][r];
           if (p.beta != 0.0) v = fma(p.beta, crow[ni * 16], v);
           crow[ni * 16] = v;
         }
       }
   } else if constexpr (EPI == EPI_ROWSQ) {
-    // out0[tj][row] = sum over this tile's 128 columns of (alpha*acc)^2
-    double* red = smem;  // [2 (wc)][128 rows]
+    // out0[tj][row] = sum over this tile's columns of (alpha*acc)^2
+    double* red = smem;  // [2 (wc)][TILE rows]
     __syncthreads();
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         double s = 0.0;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) s = fma(acc[mi][ni][r], acc[mi][ni][r], s);
+        for (int ni = 0; ni < MI; ++ni) s = fma(acc[mi][ni][r], acc[mi][ni][r], s);
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
         s += __shfl_xor(s, 4);
         s += __shfl_xor(s, 8);
-        if (lcol == 0) red[wc * 128 + wr * 64 + mi * 16 + lrow + 4 * r] = s;
+        if (lcol == 0) red[wc * TILE + wr * WT + mi * 16 + lrow + 4 * r] = s;
       }
     __syncthreads();
-    if (tid < 128)
-      p.out0[(int64_t)tj * p.ld_out + row0 + tid] = p.alpha * p.alpha * (red[tid] + red[128 + tid]);
+    if (tid < TILE)
+      p.out0[(int64_t)tj * p.ld_out + row0 + tid] = p.alpha * p.alpha * (red[tid] + red[TILE + tid]);
   } else {  // EPI_COLRED: out0[ti][col] = sum_rows w[row]*acc, out1[ti][col] = sum_rows acc^2
-    double* red = smem;  // [2 (wr)][2][128]
+    double* red = smem;  // [2 (wr)][2][TILE]
     __syncthreads();
-    double wv[4][4];
+    double wv[MI][4];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) wv[mi][r] = p.w[row0 + wr * 64 + mi * 16 + lrow + 4 * r];
+      for (int r = 0; r < 4; ++r) wv[mi][r] = p.w[row0 + wr * WT + mi * 16 + lrow + 4 * r];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
+    for (int ni = 0; ni < MI; ++ni) {
       double s1 = 0.0, s2 = 0.0;
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           s1 = fma(acc[mi][ni][r], wv[mi][r], s1);
@@ -260,41 +282,52 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       s2 += __shfl_xor(s2, 16);
       s2 += __shfl_xor(s2, 32);
       if (lrow == 0) {
-        red[wr * 256 + wc * 64 + ni * 16 + lcol] = s1;
-        red[wr * 256 + 128 + wc * 64 + ni * 16 + lcol] = s2;
+        red[wr * 2 * TILE + wc * WT + ni * 16 + lcol] = s1;
+        red[wr * 2 * TILE + TILE + wc * WT + ni * 16 + lcol] = s2;
       }
     }
     __syncthreads();
-    if (tid < 128) {
-      p.out0[(int64_t)ti * p.ld_out + col0 + tid] = p.alpha * (red[tid] + red[256 + tid]);
+    if (tid < TILE) {
+      p.out0[(int64_t)ti * p.ld_out + col0 + tid] = p.alpha * (red[tid] + red[2 * TILE + tid]);
       p.out1[(int64_t)ti * p.ld_out + col0 + tid] =
-          p.alpha * p.alpha * (red[128 + tid] + red[384 + tid]);
+          p.alpha * p.alpha * (red[TILE + tid] + red[3 * TILE + tid]);
     }
   }
 }
 
 hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipStream_t s) {
   GemmParams p = pin;
-  if (p.M % BM || p.N % BN || p.K % BK || p.M <= 0 || p.N <= 0) return hipErrorInvalidValue;
+  if (p.M % GPS_TILE || p.N % GPS_TILE || p.K % BK || p.M <= 0 || p.N <= 0)
+    return hipErrorInvalidValue;
   if ((p.lda & 1) || (p.ldb & 1) || (p.ldc & 1)) return hipErrorInvalidValue;
   if (p.lower_out && p.M != p.N) return hipErrorInvalidValue;
   if (p.ksplit < 1) p.ksplit = 1;
   if (p.ksplit > 1 && (epi != EPI_STORE || p.beta != 0.0)) return hipErrorInvalidValue;
-  p.tiles_m = p.M / BM;
-  p.tiles_n = p.N / BN;
+  // tile choice: 64×64 when a 128-tile grid would leave most of the 256 CUs idle
+  // (the bottom of the recursion); the row / column epilogue slabs are laid out
+  // per 128-tile, so those epilogues keep the 128 tile.
+  const int64_t t128 = p.lower_out ? (int64_t)(p.M / 128) * (p.M / 128 + 1) / 2
+                                   : (int64_t)(p.M / 128) * (p.N / 128);
+  const int tile = (epi == EPI_STORE && p.ksplit == 1 && t128 < 64) ? 64 : 128;
+  p.tiles_m = p.M / tile;
+  p.tiles_n = p.N / tile;
   const int tiles = p.lower_out ? p.tiles_m * (p.tiles_m + 1) / 2 : p.tiles_m * p.tiles_n;
   dim3 grid(tiles, p.ksplit), block(256);
-#define GPS_GEMM_CASE(AL, BL, EP)                                                   \
-  if (alay == AL && blay == BL && epi == EP) {                                     \
-    hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP>), grid, block, 0, s, p);       \
+#define GPS_GEMM_CASE(AL, BL, EP, T)                                               \
+  if (alay == AL && blay == BL && epi == EP && tile == T) {                        \
+    hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T>), grid, block, 0, s, p);    \
     return hipGetLastError();                                                      \
   }
-  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE)
-  GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE)
-  GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE)
-  GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE)
-  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_ROWSQ)
-  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_COLRED)
+  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE, 128)
+  GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE, 128)
+  GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE, 128)
+  GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE, 128)
+  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_ROWSQ, 128)
+  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_COLRED, 128)
+  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE, 64)
+  GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE, 64)
+  GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE, 64)
+  GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE, 64)
 #undef GPS_GEMM_CASE
   return hipErrorInvalidValue;
 }

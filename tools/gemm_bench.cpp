@@ -1,0 +1,67 @@
+// GEMM microbenchmark against libgpscore's internal launcher (gps::launch_gemm).
+//   hipcc -O3 --offload-arch=gfx950 -I<pkg>/csrc tools/gemm_bench.cpp -L<pkg>/gpscore -lgpscore -o /tmp/gb
+// Cases: square NT GEMM, the predictive TRMM shape, an L2-resident variant
+// (lda = ldb = 0: every tile re-reads the same 16 KB, isolating the in-kernel
+// pipeline from memory latency), and the recursion's small shapes.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include "gps_internal.h"
+using namespace gps;
+
+static double run(int al, int bl, int epi, GemmParams p, int reps, double flops) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  launch_gemm(al, bl, epi, p, 0);
+  hipEventRecord(e0);
+  for (int r = 0; r < reps; ++r) launch_gemm(al, bl, epi, p, 0);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  return flops * reps / (ms * 1e-3) / 1e12;
+}
+
+int main() {
+  const int64_t n = 20480;
+  double *A, *B, *C, *o0, *o1, *w;
+  hipMalloc(&A, n * n * 8); hipMalloc(&B, n * n * 8); hipMalloc(&C, n * n * 8);
+  hipMalloc(&o0, 64 * 200064 * 8); hipMalloc(&o1, 256 * n * 8); hipMalloc(&w, n * 8);
+  hipMemset(A, 0, n * n * 8); hipMemset(B, 0, n * n * 8); hipMemset(w, 0, n * 8);
+  GemmParams p; memset(&p, 0, sizeof(p)); p.alpha = 1; p.ksplit = 1;
+  struct { const char* name; int M, N, K, al, bl, epi, tri, lower, l2; } cs[] = {
+    {"NT 8192^3", 8192, 8192, 8192, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+    {"NT 8192^3 L2-resident", 8192, 8192, 8192, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 1},
+    {"NN 8192^3", 8192, 8192, 8192, LAY_N, LAY_N, EPI_STORE, TRI_NONE, 0, 0},
+    {"TN 4096x4096 K=40960", 4096, 4096, 40960 / 2, LAY_T, LAY_N, EPI_STORE, TRI_NONE, 0, 0},
+    {"SYRK NT 10112 K=9984", 10112, 10112, 9984, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 1, 0},
+    {"TRMM-colred 20096x5120", 20096, 5120, 20096, LAY_N, LAY_T, EPI_COLRED, TRI_K_LE_I, 0, 0},
+    {"TRMM-colred L2-resident", 20096, 5120, 20096, LAY_N, LAY_T, EPI_COLRED, TRI_K_LE_I, 0, 1},
+    {"NT 20096x5120x20096 store", 20096, 5120, 20096, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+    {"NT 20096x5120 tri store", 20096, 5120, 20096, LAY_N, LAY_T, EPI_STORE, TRI_K_LE_I, 0, 0},
+    {"NT 20096x5120 colred notri", 20096, 5120, 20096, LAY_N, LAY_T, EPI_COLRED, TRI_NONE, 0, 0},
+    {"NT 5120x20096x20096 store", 5120, 20096, 20096, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+    {"K_LE_J NT 10112x9984x9984", 10112, 9984, 9984, LAY_N, LAY_T, EPI_STORE, TRI_K_LE_J, 0, 0},
+    {"K_GE_J NN 10112x9984x9984", 10112, 9984, 9984, LAY_N, LAY_N, EPI_STORE, TRI_K_GE_J, 0, 0},
+    {"K_LE_I NN 10112x9984x10112", 10112, 9984, 10112, LAY_N, LAY_N, EPI_STORE, TRI_K_LE_I, 0, 0},
+    {"NT 1280^3", 1280, 1280, 1280, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+    {"NT 640x640x640", 640, 640, 640, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+    {"NT 256^3", 256, 256, 256, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+  };
+  for (auto& c : cs) {
+    p.A = A; p.B = B; p.C = C; p.w = w; p.out0 = o0; p.out1 = o1;
+    p.lda = c.l2 ? 0 : (c.al == LAY_N ? c.K : c.M);
+    p.ldb = c.l2 ? 0 : (c.bl == LAY_T ? c.K : c.N);
+    p.ldc = c.N; p.ld_out = c.epi == EPI_ROWSQ ? c.M : c.N;
+    p.M = c.M; p.N = c.N; p.K = c.K; p.tri = c.tri; p.lower_out = c.lower;
+    // every operand must lie inside its n*n allocation (an out-of-bounds read can fault the GPU)
+    if ((double)c.M * c.K > (double)n * n || (double)c.K * c.N > (double)n * n ||
+        (double)c.M * c.N > (double)n * n) { printf("%-28s skipped (too big)\n", c.name); continue; }
+    double fl = c.lower ? (double)c.M * (c.M + 1) * c.K : (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.K;
+    int reps = fl > 1e12 ? 3 : (fl > 1e10 ? 20 : 200);
+    for (int mm = 0; mm < 3; ++mm) {
+      p.map_mode = mm;
+      printf("%-28s map%d %7.2f TF/s\n", c.name, mm, run(c.al, c.bl, c.epi, p, reps, fl));
+    }
+  }
+  return 0;
+}
