@@ -114,6 +114,18 @@ def timed(ctl, ctx, fn, steps):
     return ctl.max(time.perf_counter() - t0)
 
 
+def kernel_pass(ctl, ctx, fn, steps):
+    """Time `steps` more steps with every launch bracketed by hipEvents on its own
+    (single) stream, so each launch's duration is its own (overlap off)."""
+    ctx.set_overlap(False)
+    ctx.prof(True)
+    t = timed(ctl, ctx, fn, steps)
+    prof = ctx.prof_collect()
+    ctx.prof(False)
+    ctx.set_overlap(True)
+    return prof, 1e3 * t / steps
+
+
 def kernel_summary(prof, steps):
     """per-step kernel stats from the library's hipEvent records."""
     out = {}
@@ -124,10 +136,10 @@ def kernel_summary(prof, steps):
     return out
 
 
-def roofline_mfma(prof, traffic=None):
-    f = sum(v["flop"] for k, v in prof.items() if k.startswith("gemm"))
-    ms = sum(v["ms"] for k, v in prof.items() if k.startswith("gemm"))
-    n = sum(v["count"] for k, v in prof.items() if k.startswith("gemm"))
+def roofline_mfma(prof, traffic=None, steps=1):
+    f = sum(v["flop"] for k, v in prof.items() if k.startswith("gemm")) / steps
+    ms = sum(v["ms"] for k, v in prof.items() if k.startswith("gemm")) / steps
+    n = sum(v["count"] for k, v in prof.items() if k.startswith("gemm")) / steps
     ach = f / (ms * 1e-3) / 1e12 if ms else 0.0
     return {"bound": "mfma", "kernel": "gemm_f64_kernel (all launches of the step)",
             "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
@@ -136,13 +148,14 @@ def roofline_mfma(prof, traffic=None):
             "flop_per_launch": f / n if n else None}
 
 
-def roofline_gram(prof, tags=("gram_kff", "gram_ksf")):
-    b = sum(prof[t]["bytes"] for t in tags if t in prof)
-    ms = sum(prof[t]["ms"] for t in tags if t in prof)
+def roofline_gram(prof, steps=1, traffic=None, tags=("gram_kff", "gram_ksf")):
+    b = sum(prof[t]["bytes"] for t in tags if t in prof) / steps
+    ms = sum(prof[t]["ms"] for t in tags if t in prof) / steps
     ach = b / (ms * 1e-3) / 1e9 if ms else 0.0
     return {"bound": "hbm", "kernel": "gram_kernel<8> (K_ff lower + K*f)", "achieved": round(ach, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-            "traffic": None, "bytes_per_step": b}
+            "traffic": traffic, "bytes_per_step": b,
+            "bytes_per_launch": b / max(1, sum(1 for t in tags if t in prof))}
 
 
 def cpu_baseline():
@@ -193,20 +206,23 @@ def main():
 
     for _ in range(args.warmup):
         unit()
-    ctx.prof(True)
+    # headline pass: production configuration (side-stream overlap on, no events)
     t_full = timed(ctl, ctx, unit, args.steps)
-    prof = ctx.prof_collect()
-    ctx.prof(False)
     ms_full = 1e3 * t_full / args.steps
+    # kernel-accounting pass: same steps, one stream, hipEvents around every launch
+    prof, ms_acct = kernel_pass(ctl, ctx, unit, args.steps)
     obj = gp.fit(theta=th, return_loo=False).objectives
     _, _, sc = gp.predict(with_scores=True)
 
-    traffic = None
+    # HBM bytes per launch from the committed rocprofv3 counter passes
+    # (tools/profile_round.sh -> tools/traffic.py; counters cannot be read live here)
+    traffic = traffic_gram = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("gemm_per_launch_bytes")
+            tr = json.load(open(args.traffic_json)).get("_roofline", {})
+            traffic, traffic_gram = tr.get("gemm_per_launch_bytes"), tr.get("gram_per_launch_bytes")
         except Exception:
-            traffic = None
+            traffic = traffic_gram = None
 
     res = {
         "metric": METRIC,
@@ -219,10 +235,12 @@ def main():
         "config": {"workload": f"{args.config} full GP fit(NLML+LOO-CRPS+LOO-LogS)+predict+score",
                    "n": c["n"], "d": c["d"], "n_test": c["nt"], "kernel": "ARD",
                    "parallelism": "replicas" if world > 1 else "single"},
-        "roofline": roofline_mfma(prof, traffic),
-        "roofline_gram": roofline_gram(prof),
+        "roofline": roofline_mfma(prof, traffic, args.steps),
+        "roofline_gram": roofline_gram(prof, args.steps, traffic_gram),
         "objectives": obj, "scores": sc,
         "kernels_per_step": kernel_summary(prof, args.steps),
+        "kernel_accounting": {"ms_per_step": ms_acct, "streams": 1,
+                              "note": "second timed pass, overlap off, hipEvents around each launch"},
     }
 
     # ---------------- FITC (rows sharded, RCCL all-reduce) ----------------
@@ -257,10 +275,8 @@ def main():
 
             for _ in range(args.warmup):
                 funit()
-            ctx.prof(True)
             tf = timed(ctl, ctx, funit, args.steps)
-            fprof = ctx.prof_collect()
-            ctx.prof(False)
+            fprof, fms_acct = kernel_pass(ctl, ctx, funit, args.steps)
             fobj = fgp.fit(theta=thf, return_loo=False).objectives
             fitc[leg] = {"ms_per_step": 1e3 * tf / args.steps,
                          "units_per_s": args.steps / tf,
@@ -268,7 +284,8 @@ def main():
                                     "rows_per_rank": b - a, "ranks": world},
                          "scaling": "strong",
                          "objectives": fobj,
-                         "roofline": roofline_mfma(fprof),
+                         "roofline": roofline_mfma(fprof, None, args.steps),
+                         "kernel_accounting_ms_per_step": fms_acct,
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             del Xf, yf, Xtf, ytf
         if world > 1:

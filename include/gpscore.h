@@ -60,6 +60,13 @@ int gps_ctx_set_stream(gps_ctx* ctx, void* hip_stream);
 void* gps_ctx_stream(gps_ctx* ctx);
 int gps_ctx_synchronize(gps_ctx* ctx);
 
+/* ---- options ---------------------------------------------------------------- */
+enum {
+  GPS_OPT_OVERLAP = 0  /* 1 (default): off-critical-path GEMMs of the factorisation run on a
+                          second HIP stream; 0: everything on one stream (clean per-kernel timing) */
+};
+int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
+
 /* ---- per-kernel timing (hipEvents on the ctx stream) ---------------------- */
 int gps_prof_enable(gps_ctx* ctx, int on);
 /* Synchronises, then writes a JSON object {tag: {count, ms, flop, bytes}} and clears. */

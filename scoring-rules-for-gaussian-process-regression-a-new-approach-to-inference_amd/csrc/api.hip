@@ -60,6 +60,10 @@ struct gps_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = true;
+  hipStream_t side = nullptr;          // second stream for off-critical-path GEMMs
+  bool overlap = true;                 // GPS_OPT_OVERLAP
+  std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
+  size_t sync_used = 0;
   std::string err;
   // profiling
   bool prof = false;
@@ -156,20 +160,32 @@ int get_event(gps_ctx* c) {
 
 struct Prof {
   gps_ctx* c;
+  hipStream_t st;
   int e0 = -1;
   const char* tag;
   double flop, bytes;
-  Prof(gps_ctx* c_, const char* t, double f, double b) : c(c_), tag(t), flop(f), bytes(b) {
-    if (c->prof && (e0 = get_event(c)) >= 0) (void)hipEventRecord(c->ev[e0], c->stream);
+  Prof(gps_ctx* c_, const char* t, double f, double b, hipStream_t s_ = nullptr)
+      : c(c_), st(s_ ? s_ : c_->stream), tag(t), flop(f), bytes(b) {
+    if (c->prof && (e0 = get_event(c)) >= 0) (void)hipEventRecord(c->ev[e0], st);
   }
   ~Prof() {
     if (!c->prof || e0 < 0) return;
     const int e1 = get_event(c);
     if (e1 < 0) return;
-    (void)hipEventRecord(c->ev[e1], c->stream);
+    (void)hipEventRecord(c->ev[e1], st);
     c->recs.push_back({tag, e0, e1, flop, bytes});
   }
 };
+
+// fork/join event from a per-call pool (reset by potrf_inv)
+hipEvent_t sync_event(gps_ctx* c) {
+  if (c->sync_used == c->sync_ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    c->sync_ev.push_back(e);
+  }
+  return c->sync_ev[c->sync_used++];
+}
 
 // --------------------------------------------------------------- launch helpers
 GemmParams gp0() {
@@ -203,9 +219,10 @@ double gemm_flops(const GemmParams& p) {
   return 2.0 * M * N * K;
 }
 
-int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p) {
-  Prof pr(ctx, gemm_tag(al, bl, epi, p), gemm_flops(p), 0);
-  HIPCHK(launch_gemm(al, bl, epi, p, ctx->stream));
+int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t st = nullptr) {
+  if (!st) st = ctx->stream;
+  Prof pr(ctx, gemm_tag(al, bl, epi, p), gemm_flops(p), 0, st);
+  HIPCHK(launch_gemm(al, bl, epi, p, st));
   return 0;
 }
 
@@ -234,7 +251,11 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
   return 0;
 }
 
-// recursive Cholesky + inverse on a padded (multiple of 128) SPD block
+// recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
+// W is this level's workspace (n1·n2 doubles); deeper levels on the A22 side get
+// the region after it, so the side-stream GEMM that still reads this level's W
+// never races with them.  T = L21 L11⁻¹ only feeds the final L⁻¹21 product, so it
+// runs on ctx->side concurrently with the SYRK and rec(A22) (fork / join events).
 int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
                   int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
                   int64_t ldlo) {
@@ -261,21 +282,32 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   }
   if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
                                     (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
+  // fork: T = L21 · L11⁻¹ → A21 on the side stream
+  hipStream_t ts = ctx->overlap ? ctx->side : s;
+  hipEvent_t fork = sync_event(ctx), join = sync_event(ctx);
+  if (!fork || !join) return fail(ctx, -2, "hipEventCreate failed");
+  if (ctx->overlap) {
+    HIPCHK(hipEventRecord(fork, s));
+    HIPCHK(hipStreamWaitEvent(ts, fork, 0));
+  }
+  {
+    GemmParams p = gp0();
+    p.A = W; p.lda = n1; p.B = Linv; p.ldb = ldl; p.C = A21; p.ldc = lda;
+    p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, ts))) return rc;
+  }
+  if (ctx->overlap) HIPCHK(hipEventRecord(join, ts));
   {  // A22 -= L21 L21ᵀ  (lower tiles)
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
     p.M = n2; p.N = n2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
   }
-  {  // T = L21 · L11⁻¹  → A21
-    GemmParams p = gp0();
-    p.A = W; p.lda = n1; p.B = Linv; p.ldb = ldl; p.C = A21; p.ldc = lda;
-    p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
-    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
-  }
-  if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W, n2b, logdiag + n1, info, base + n1,
-                          nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr, ldlo)))
+  if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W + (int64_t)n1 * n2, n2b, logdiag + n1, info,
+                          base + n1, nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr,
+                          ldlo)))
     return rc;
+  if (ctx->overlap) HIPCHK(hipStreamWaitEvent(s, join, 0));
   {  // L⁻¹21 = −L22⁻¹ · T
     GemmParams p = gp0();
     p.A = Li22; p.lda = ldl; p.B = A21; p.ldb = lda; p.C = Li21; p.ldc = ldl;
@@ -285,10 +317,15 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   return 0;
 }
 
+// workspace of potrf_inv_rec: this level's n1·n2 plus, recursively, the A22 side
 size_t potrf_ws_doubles(int64_t n_pad) {
-  const int64_t nb = n_pad / GPS_TILE;
-  const int64_t n1 = (nb / 2) * GPS_TILE, n2 = n_pad - n1;
-  return (size_t)std::max<int64_t>(n1 * n2, GPS_TILE * GPS_TILE);
+  int64_t nb = n_pad / GPS_TILE, tot = 0;
+  while (nb > 1) {
+    const int64_t n1 = (nb / 2) * GPS_TILE, n2 = (nb - nb / 2) * GPS_TILE;
+    tot += n1 * n2;
+    nb = nb - nb / 2;
+  }
+  return (size_t)std::max<int64_t>(tot, GPS_TILE * GPS_TILE);
 }
 
 // factor the padded SPD matrix in A (destroyed) into Linv (must be zero in strict-upper
@@ -300,6 +337,7 @@ int reset_info(gps_ctx* ctx) {
 
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
+  ctx->sync_used = 0;
   int rc = potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
                          static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad);
   return rc;
@@ -377,6 +415,7 @@ int gps_ctx_create(int device, gps_ctx** out) {
   ctx->device = device;
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HIPCHK(hipHostMalloc((void**)&ctx->hsmall, 256 * sizeof(double), hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&ctx->hinfo, 16, hipHostMallocDefault));
   HIPCHK(ensure(ctx->info, 16));
@@ -401,6 +440,8 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->hsmall) (void)hipHostFree(ctx->hsmall);
   if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -422,6 +463,14 @@ int gps_ctx_set_stream(gps_ctx* ctx, void* hip_stream) {
     ctx->own_stream = true;
   }
   return 0;
+}
+
+int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
+  if (int rc = bind(ctx)) return rc;
+  switch (key) {
+    case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
+    default: return fail(ctx, -1, "unknown option");
+  }
 }
 
 void* gps_ctx_stream(gps_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }

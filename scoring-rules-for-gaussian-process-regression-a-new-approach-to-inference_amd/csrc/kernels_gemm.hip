@@ -88,7 +88,9 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   constexpr int MI = WT / 16;            // MFMA blocks per wave edge
   constexpr int PER = TILE * BK / 256;   // doubles of one operand slice per thread (8 or 4)
   constexpr int NQ = PER / 2;            // 16-byte loads per operand per thread
-  constexpr int TPR = TILE / PER;        // threads per k-row for k-major sources
+  constexpr int TPR = TILE / PER;        // threads per k-row for k-major sources (each thread
+                                         // owns NQ 16-byte chunks 2·TPR doubles apart, so a
+                                         // ds_write_b128 covers contiguous bytes: no conflicts)
   constexpr int TPI = BK / PER;          // threads per i-row for i-major sources
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -120,10 +122,10 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   double2 ra[NQ], rb[NQ];
   auto load_tile = [&](int k0) {
     if constexpr (ALAY == LAY_T) {  // A stored [k][i]
-      const int k = tid / TPR, i = (tid % TPR) * PER;
+      const int k = tid / TPR, i = (tid % TPR) * 2;
       const double2* src = reinterpret_cast<const double2*>(p.A + (int64_t)(k0 + k) * p.lda + row0 + i);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) ra[q] = src[q];
+      for (int q = 0; q < NQ; ++q) ra[q] = src[q * TPR];
       if (p.kscale) {
         const double sc = p.kscale[k0 + k];
 #pragma unroll
@@ -143,10 +145,10 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       }
     }
     if constexpr (BLAY == LAY_N) {  // B stored [k][j]
-      const int k = tid / TPR, j = (tid % TPR) * PER;
+      const int k = tid / TPR, j = (tid % TPR) * 2;
       const double2* src = reinterpret_cast<const double2*>(p.B + (int64_t)(k0 + k) * p.ldb + col0 + j);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) rb[q] = src[q];
+      for (int q = 0; q < NQ; ++q) rb[q] = src[q * TPR];
     } else {  // B stored [j][k]
       const int j = tid / TPI, k = (tid % TPI) * PER;
       const double2* src = reinterpret_cast<const double2*>(p.B + (int64_t)(col0 + j) * p.ldb + k0 + k);
@@ -158,9 +160,9 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     double* As = smem + buf * STAGE;
     double* Bs = As + BK * LS;
     if constexpr (ALAY == LAY_T) {
-      const int k = tid / TPR, i = (tid % TPR) * PER;
+      const int k = tid / TPR, i = (tid % TPR) * 2;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&As[k * LS + i + 2 * q]) = ra[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&As[k * LS + i + 2 * TPR * q]) = ra[q];
     } else {
       const int i = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll
@@ -170,9 +172,9 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       }
     }
     if constexpr (BLAY == LAY_N) {
-      const int k = tid / TPR, j = (tid % TPR) * PER;
+      const int k = tid / TPR, j = (tid % TPR) * 2;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&Bs[k * LS + j + 2 * q]) = rb[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&Bs[k * LS + j + 2 * TPR * q]) = rb[q];
     } else {
       const int j = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll

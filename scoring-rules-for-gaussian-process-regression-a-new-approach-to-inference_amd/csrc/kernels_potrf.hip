@@ -6,10 +6,10 @@
 // sub-blocks do arithmetic.  The block is processed in 32 panel steps of width 4:
 //
 //   factor, step jb (two barriers):
-//     1. thread (jb, jb) factors its 4×4 diagonal block in registers, inverts
-//        it (D⁻¹), records log L_ii (the ½log|A| terms of KF:332) and the first
-//        non-positive pivot (torch.potrf's "leading minor not PD"), and
-//        publishes L_jj and D⁻¹ to LDS;
+//     1. thread (jb, jb) factors its 4×4 diagonal block in registers (one
+//        rsqrt per pivot, no divisions: this is the serial critical path),
+//        inverts it (D⁻¹), records the first non-positive pivot (torch.potrf's
+//        "leading minor not PD"), and publishes L_jj and D⁻¹ to LDS;
 //     2. the panel threads (br > jb, bc = jb) form L_rb = A_rb D⁻ᵀ and publish it;
 //     3. every trailing thread (br >= bc > jb) applies the rank-4 update
 //        A_rc -= L_rb L_cbᵀ from LDS.  The diagonal thread of step jb+1 finishes
@@ -18,7 +18,8 @@
 //     X = I held in the same registers: block row ib is finalised
 //     X_ib ← D_ib⁻¹ X_ib and published, then every block row r > ib does
 //     X_r -= L_r,ib X_ib.
-// L is kept transposed in LDS (LT[col][row], 132-double rows) so a thread's
+// log L_ii (the ½log|A| terms of KF:332) is taken for all 128 pivots in parallel
+// after the factorisation.  L is kept transposed in LDS (LT[col][row], 132-double rows) so a thread's
 // 4-row slice of an L column is one contiguous 32-byte read.
 #include "gps_internal.h"
 
@@ -62,31 +63,38 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restri
   // ======================= factorisation =======================
   for (int jb = 0; jb < 32; ++jb) {
     if (br == jb && bc == jb) {
-      // 4×4 Cholesky in registers
+      // 4×4 Cholesky in registers: one rsqrt per pivot, no divisions on this
+      // serial path (it is the per-step critical path of the whole block)
+      double is[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const double d = a[j][j];
         if (!(d > 0.0) && 4 * jb + j < nreal) atomicMin(info, base + 4 * jb + j + 1);
-        const double s = sqrt(d), is = 1.0 / s;
-        a[j][j] = s;
-        logdiag[4 * jb + j] = log(s);
+        is[j] = rsqrt(d);
+        a[j][j] = d * is[j];
 #pragma unroll
-        for (int r = j + 1; r < 4; ++r) a[r][j] *= is;
+        for (int r = j + 1; r < 4; ++r) a[r][j] *= is[j];
 #pragma unroll
         for (int r = j + 1; r < 4; ++r)
 #pragma unroll
           for (int c = j + 1; c <= r; ++c) a[r][c] = fma(-a[r][j], a[c][j], a[r][c]);
       }
-      // D⁻¹ by forward substitution
+      // D⁻¹ by forward substitution, x_rc = -(1/L_rr) Σ_{c<=k<r} L_rk x_kc, x_cc = 1/L_cc
       double x[4][4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          double s = (r == c) ? 1.0 : 0.0;
+          if (r < c) {
+            x[r][c] = 0.0;
+          } else if (r == c) {
+            x[r][c] = is[r];
+          } else {
+            double t = 0.0;
 #pragma unroll
-          for (int k = 0; k < r; ++k) s = fma(-a[r][k], x[k][c], s);
-          x[r][c] = (r >= c) ? s / a[r][r] : 0.0;
+            for (int k = c; k < r; ++k) t = fma(a[r][k], x[k][c], t);
+            x[r][c] = -t * is[r];
+          }
         }
       }
 #pragma unroll
@@ -140,6 +148,7 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restri
     }
   }
   __syncthreads();
+  if (tid < NB) logdiag[tid] = log(LT[tid * LTS + tid]);
 
   if (Lout) {
     for (int e = tid; e < NB * NB / 2; e += 1024) {

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
+GPS_OPT_OVERLAP = 0
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
@@ -33,6 +34,7 @@ SIGNATURES = {
     "gps_ctx_set_stream": (_c_int, [_c_vp, _c_vp]),
     "gps_ctx_stream": (_c_vp, [_c_vp]),
     "gps_ctx_synchronize": (_c_int, [_c_vp]),
+    "gps_ctx_set_option": (_c_int, [_c_vp, _c_int, _c_int]),
     "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
     "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
     "gps_gram": (_c_int, [_c_vp, _c_int, _P, _c_i64, _P, _c_i64, _c_int, _c_dbl, _P, _c_int,
@@ -149,6 +151,10 @@ class Context:
         buf = ctypes.create_string_buffer(1 << 16)
         self.call("gps_prof_collect", buf, len(buf))
         return json.loads(buf.value.decode())
+
+    def set_overlap(self, on=True):
+        """Run the factorisation's off-critical-path GEMMs on a second stream."""
+        self.call("gps_ctx_set_option", GPS_OPT_OVERLAP, 1 if on else 0)
 
     def synchronize(self):
         self.call("gps_ctx_synchronize")
