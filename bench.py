@@ -78,7 +78,20 @@ class Ctl:
         if world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")
+            # gloo prints a "[Gloo] Rank i is connected ..." banner on fd 1; keep stdout
+            # to the one JSON line rank 0 emits
+            sys.stdout.flush()
+            saved = os.dup(1)
+            devnull = os.open(os.devnull, os.O_WRONLY)
+            os.dup2(devnull, 1)
+            try:
+                dist.init_process_group("gloo")
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(devnull)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -186,12 +199,15 @@ def main():
     ap.add_argument("--no-fitc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
+                         "no RCCL communicator (FITC objectives then cover the local shard only)")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
     ctl = Ctl(world)
     import gpscore
-    ctx = gpscore.Context(local)
+    ctx = gpscore.Context(0 if args.rehearse else local)
     gp = gpscore.GP(ctx=ctx)
 
     # ---------------- full GP (replicas) ----------------
@@ -249,7 +265,7 @@ def main():
         fitc = {}
         legs = ["C5"] + (["C4"] if world == 1 else [])
         fgp = gpscore.GP(ctx=ctx)
-        if world > 1:
+        if world > 1 and not args.rehearse:
             import ctypes
             lib = gpscore.load()
             uid = None
@@ -288,7 +304,7 @@ def main():
                          "kernel_accounting_ms_per_step": fms_acct,
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             del Xf, yf, Xtf, ytf
-        if world > 1:
+        if world > 1 and not args.rehearse:
             ctx.call("gps_comm_destroy")
         res["fitc"] = fitc
 
@@ -296,6 +312,8 @@ def main():
         cb = cpu_baseline()
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
+    if args.rehearse:
+        res["rehearsal"] = "all ranks on device 0, no RCCL: not a measurement"
     if rank == 0:
         print(json.dumps(res))
     if ctl.dist:
