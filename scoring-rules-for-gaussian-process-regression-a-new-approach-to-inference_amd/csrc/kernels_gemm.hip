@@ -35,6 +35,10 @@
 namespace gps {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+// staging registers: a native vector type, not HIP's double2 struct — struct copies
+// lower to memcpy through a private alloca that SROA cannot promote, which put the
+// B staging registers in scratch (80 B/lane of spills in the k-major-B kernels)
+typedef double dv2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 16;
 constexpr int GROUP_M = 8;
@@ -98,6 +102,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
 
   int ti, tj;
   const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
+  // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
   tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj);
   const int row0 = ti * TILE, col0 = tj * TILE;
 
@@ -119,11 +124,11 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   const int nk = ke > kb ? (ke - kb) / BK : 0;
 
   // ---- global -> register staging (PER doubles of A and of B per thread) ----
-  double2 ra[NQ], rb[NQ];
+  dv2 ra[NQ], rb[NQ];
   auto load_tile = [&](int k0) {
     if constexpr (ALAY == LAY_T) {  // A stored [k][i]
       const int k = tid / TPR, i = (tid % TPR) * 2;
-      const double2* src = reinterpret_cast<const double2*>(p.A + (int64_t)(k0 + k) * p.lda + row0 + i);
+      const dv2* src = reinterpret_cast<const dv2*>(p.A + (int64_t)(k0 + k) * p.lda + row0 + i);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) ra[q] = src[q * TPR];
       if (p.kscale) {
@@ -133,7 +138,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       }
     } else {  // A stored [i][k]
       const int i = tid / TPI, k = (tid % TPI) * PER;
-      const double2* src = reinterpret_cast<const double2*>(p.A + (int64_t)(row0 + i) * p.lda + k0 + k);
+      const dv2* src = reinterpret_cast<const dv2*>(p.A + (int64_t)(row0 + i) * p.lda + k0 + k);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) ra[q] = src[q];
       if (p.kscale) {
@@ -146,12 +151,12 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     }
     if constexpr (BLAY == LAY_N) {  // B stored [k][j]
       const int k = tid / TPR, j = (tid % TPR) * 2;
-      const double2* src = reinterpret_cast<const double2*>(p.B + (int64_t)(k0 + k) * p.ldb + col0 + j);
+      const dv2* src = reinterpret_cast<const dv2*>(p.B + (int64_t)(k0 + k) * p.ldb + col0 + j);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) rb[q] = src[q * TPR];
     } else {  // B stored [j][k]
       const int j = tid / TPI, k = (tid % TPI) * PER;
-      const double2* src = reinterpret_cast<const double2*>(p.B + (int64_t)(col0 + j) * p.ldb + k0 + k);
+      const dv2* src = reinterpret_cast<const dv2*>(p.B + (int64_t)(col0 + j) * p.ldb + k0 + k);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) rb[q] = src[q];
     }
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     if constexpr (ALAY == LAY_T) {
       const int k = tid / TPR, i = (tid % TPR) * 2;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&As[k * LS + i + 2 * TPR * q]) = ra[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<dv2*>(&As[k * LS + i + 2 * TPR * q]) = ra[q];
     } else {
       const int i = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     if constexpr (BLAY == LAY_N) {
       const int k = tid / TPR, j = (tid % TPR) * 2;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *reinterpret_cast<double2*>(&Bs[k * LS + j + 2 * TPR * q]) = rb[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<dv2*>(&Bs[k * LS + j + 2 * TPR * q]) = rb[q];
     } else {
       const int j = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll

@@ -34,6 +34,10 @@ __device__ __forceinline__ void lds_read4(const double* p, double (&v)[4]) {
   v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
 }
 
+#ifdef GPS_DIAG_STAMPS
+__device__ unsigned long long gps_stamps[32 * 8 * 17];
+#endif
+
 __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restrict__ A, int64_t lda,
                                                           double* __restrict__ Linv, int64_t ldl,
                                                           double* __restrict__ Lout, int64_t ldlo,
@@ -60,9 +64,25 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restri
     }
   }
 
+#ifndef GPS_DIAG_ABLATE
+#define GPS_DIAG_ABLATE 0  // tools/diag_bench.cpp: 1 skip pivot math, 2 skip updates, 3 skip inverse
+#endif
+#ifdef GPS_DIAG_STAMPS
+#define STAMP(slot)                                                                    \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    unsigned long long _t;                                                             \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    if ((tid & 63) == 0 || tid == 33 * jb) gps_stamps[(jb * 8 + (slot)) * 17 + (tid == 33 * jb ? 16 : (tid >> 6))] = _t; \
+  } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
   // ======================= factorisation =======================
   for (int jb = 0; jb < 32; ++jb) {
-    if (br == jb && bc == jb) {
+    STAMP(0);
+    if (br == jb && bc == jb && GPS_DIAG_ABLATE != 1) {
       // 4×4 Cholesky in registers: one rsqrt per pivot, no divisions on this
       // serial path (it is the per-step critical path of the whole block)
       double is[4];
@@ -105,7 +125,9 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restri
           LT[(c0 + c) * LTS + r0 + r] = (c <= r) ? a[r][c] : 0.0;
         }
     }
+    STAMP(1);
     __syncthreads();
+    STAMP(2);
     if (lower && bc == jb && br > jb) {  // panel: L_rb = A_rb D⁻ᵀ
       double di[4][4];
 #pragma unroll
@@ -128,8 +150,10 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restri
           LT[(c0 + c) * LTS + r0 + r] = l[r][c];
         }
     }
+    STAMP(3);
     __syncthreads();
-    if (lower && bc > jb) {  // trailing rank-4 update
+    STAMP(4);
+    if (lower && bc > jb && GPS_DIAG_ABLATE != 2) {  // trailing rank-4 update
       double lr[4][4], lc[4][4];  // [k][r]
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -165,7 +189,7 @@ __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restri
 #pragma unroll
     for (int c = 0; c < 4; ++c) a[r][c] = (r0 + r == c0 + c) ? 1.0 : 0.0;
 
-  for (int ib = 0; ib < 32; ++ib) {
+  for (int ib = 0; ib < (GPS_DIAG_ABLATE == 3 ? 0 : 32); ++ib) {
     double* xb = XB + (ib & 1) * 4 * NB;
     if (lower && br == ib) {  // X_ib ← D_ib⁻¹ X_ib, publish
       double di[4][4];

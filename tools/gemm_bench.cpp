@@ -6,8 +6,17 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 #include "gps_internal.h"
 using namespace gps;
+
+__global__ void fill_rand(double* p, int64_t n, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t x = (i + 1) * 0x9E3779B97F4A7C15ull ^ seed;
+    x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29;
+    p[i] = (double)(x >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+  }
+}
 
 static double run(int al, int bl, int epi, GemmParams p, int reps, double flops) {
   hipEvent_t e0, e1;
@@ -26,7 +35,14 @@ int main() {
   double *A, *B, *C, *o0, *o1, *w;
   hipMalloc(&A, n * n * 8); hipMalloc(&B, n * n * 8); hipMalloc(&C, n * n * 8);
   hipMalloc(&o0, 64 * 200064 * 8); hipMalloc(&o1, 256 * n * 8); hipMalloc(&w, n * 8);
-  hipMemset(A, 0, n * n * 8); hipMemset(B, 0, n * n * 8); hipMemset(w, 0, n * 8);
+  const bool zeros = getenv("GB_ZEROS") != nullptr;
+  if (zeros) { hipMemset(A, 0, n * n * 8); hipMemset(B, 0, n * n * 8); }
+  else {
+    hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, A, n * n, 1ull);
+    hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, B, n * n, 2ull);
+  }
+  hipMemset(w, 0, n * 8);
+  printf("operands: %s\n", zeros ? "zeros" : "uniform random [-0.5, 0.5)");
   GemmParams p; memset(&p, 0, sizeof(p)); p.alpha = 1; p.ksplit = 1;
   struct { const char* name; int M, N, K, al, bl, epi, tri, lower, l2; } cs[] = {
     {"NT 8192^3", 8192, 8192, 8192, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
@@ -43,6 +59,9 @@ int main() {
     {"K_LE_J NT 10112x9984x9984", 10112, 9984, 9984, LAY_N, LAY_T, EPI_STORE, TRI_K_LE_J, 0, 0},
     {"K_GE_J NN 10112x9984x9984", 10112, 9984, 9984, LAY_N, LAY_N, EPI_STORE, TRI_K_GE_J, 0, 0},
     {"K_LE_I NN 10112x9984x10112", 10112, 9984, 10112, LAY_N, LAY_N, EPI_STORE, TRI_K_LE_I, 0, 0},
+    {"SYRK NT 5120 K=5120", 5120, 5120, 5120, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 1, 0},
+    {"NT 5120^3", 5120, 5120, 5120, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
+    {"NT 2560^3", 2560, 2560, 2560, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
     {"NT 1280^3", 1280, 1280, 1280, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
     {"NT 640x640x640", 640, 640, 640, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
     {"NT 256^3", 256, 256, 256, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
@@ -59,6 +78,7 @@ int main() {
     double fl = c.lower ? (double)c.M * (c.M + 1) * c.K : (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.K;
     int reps = fl > 1e12 ? 3 : (fl > 1e10 ? 20 : 200);
     for (int mm = 0; mm < 3; ++mm) {
+      if (!c.tri && !c.lower && mm) continue;
       p.map_mode = mm;
       printf("%-28s map%d %7.2f TF/s\n", c.name, mm, run(c.al, c.bl, c.epi, p, reps, fl));
     }
