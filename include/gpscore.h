@@ -67,7 +67,7 @@ enum {
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
-/* ---- per-kernel timing (hipEvents on the ctx stream) ---------------------- */
+/* on: 0 off, 1 per-kernel-class tags, 2 GEMM tags also carry layout/shape/tri/split-K/lda */
 int gps_prof_enable(gps_ctx* ctx, int on);
 /* Synchronises, then writes a JSON object {tag: {count, ms, flop, bytes}} and clears. */
 int gps_prof_collect(gps_ctx* ctx, char* json_out, int64_t cap);

@@ -66,7 +66,7 @@ struct gps_ctx {
   size_t sync_used = 0;
   std::string err;
   // profiling
-  bool prof = false;
+  int prof = 0;  // 1: per-tag timing, 2: per-shape tags
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
   std::vector<ProfRec> recs;
@@ -98,6 +98,8 @@ struct gps_ctx {
   int nranks = 1, rank = 0;
   // ---- compat scratch (gps_gram / potrf / potrs / diag_inv / scores)
   DBuf t0, t1, t2, t3, t4;
+  // ---- split-K slabs, one per stream (GEMMs on the two streams run concurrently)
+  DBuf ws_main, ws_side;
 };
 
 namespace {
@@ -162,9 +164,9 @@ struct Prof {
   gps_ctx* c;
   hipStream_t st;
   int e0 = -1;
-  const char* tag;
+  std::string tag;
   double flop, bytes;
-  Prof(gps_ctx* c_, const char* t, double f, double b, hipStream_t s_ = nullptr)
+  Prof(gps_ctx* c_, std::string t, double f, double b, hipStream_t s_ = nullptr)
       : c(c_), st(s_ ? s_ : c_->stream), tag(t), flop(f), bytes(b) {
     if (c->prof && (e0 = get_event(c)) >= 0) (void)hipEventRecord(c->ev[e0], st);
   }
@@ -188,6 +190,8 @@ hipEvent_t sync_event(gps_ctx* c) {
 }
 
 // --------------------------------------------------------------- launch helpers
+constexpr int64_t kSplitWsDoubles = 32ll << 20;  // 256 MiB of split-K slabs per stream
+
 GemmParams gp0() {
   GemmParams p;
   memset(&p, 0, sizeof(p));
@@ -221,8 +225,23 @@ double gemm_flops(const GemmParams& p) {
 
 int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t st = nullptr) {
   if (!st) st = ctx->stream;
-  Prof pr(ctx, gemm_tag(al, bl, epi, p), gemm_flops(p), 0, st);
-  HIPCHK(launch_gemm(al, bl, epi, p, st));
+  GemmParams q = p;
+  if (epi == EPI_STORE && q.ksplit == 1 && !q.ws) {  // let gemm_plan split K on small grids
+    DBuf& ws = st == ctx->side ? ctx->ws_side : ctx->ws_main;
+    HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8));
+    q.ws = ws.d();
+    q.ws_cap = kSplitWsDoubles;
+  }
+  std::string tag = gemm_tag(al, bl, epi, p);
+  if (ctx->prof > 1) {  // per-shape accounting (gps_prof_enable(ctx, 2))
+    const GemmPlan plan = gemm_plan(epi, q, q.ws ? q.ws_cap : 0);
+    char buf[160];
+    snprintf(buf, sizeof(buf), " %c%c %dx%dx%d tri%d t%d ks%d ld%lld", al ? 'T' : 'N',
+             bl ? 'T' : 'N', p.M, p.N, p.K, (int)p.tri, plan.tile, plan.ksplit, (long long)p.lda);
+    tag += buf;
+  }
+  Prof pr(ctx, tag, gemm_flops(p), 0, st);
+  HIPCHK(launch_gemm(al, bl, epi, q, st));
   return 0;
 }
 
@@ -437,7 +456,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
                  &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
-                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4};
+                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
@@ -483,7 +502,7 @@ int gps_ctx_synchronize(gps_ctx* ctx) {
 
 int gps_prof_enable(gps_ctx* ctx, int on) {
   if (int rc = bind(ctx)) return rc;
-  ctx->prof = on != 0;
+  ctx->prof = on;
   return 0;
 }
 

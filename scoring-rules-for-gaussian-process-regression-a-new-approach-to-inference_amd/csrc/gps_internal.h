@@ -58,7 +58,14 @@ struct GemmParams {
   int tri;
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap
+  int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
+  double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
+  int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
 };
+
+// launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
+struct GemmPlan { int tile, ksplit; };
+GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 
 // ------------------------------------------------------------------ launchers
 hipError_t launch_gram(const GramParams& p, hipStream_t s);

@@ -302,6 +302,51 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   }
 }
 
+// C = beta*C + alpha * sum_s slab_s, slabs summed in slice order (deterministic);
+// lower_tile > 0: only tiles with tj <= ti at that tile edge (the rest of a SYRK slab is unwritten)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __restrict__ ws, int ks,
+                                                            int M, int N, int lower_tile,
+                                                            double alpha, double beta,
+                                                            double* __restrict__ C, int64_t ldc) {
+  const int64_t e = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (e >= (int64_t)M * N) return;
+  const int i = (int)(e / N), j = (int)(e - (int64_t)i * N);
+  if (lower_tile && j / lower_tile > i / lower_tile) return;
+  const int64_t slab = (int64_t)M * N;
+  dv2 s = *reinterpret_cast<const dv2*>(ws + e);
+  for (int q = 1; q < ks; ++q) s += *reinterpret_cast<const dv2*>(ws + q * slab + e);
+  dv2* c = reinterpret_cast<dv2*>(C + (int64_t)i * ldc + j);
+  dv2 v = alpha * s;
+  if (beta != 0.0) v += beta * *c;
+  *c = v;
+}
+
+static int64_t tiles_for(const GemmParams& p, int tile) {
+  const int64_t tm = p.M / tile, tn = p.N / tile;
+  return p.lower_out ? tm * (tm + 1) / 2 : tm * tn;
+}
+
+// Launch shape.  The 128-tile kernel holds 2 workgroups per CU (512 slots on 256 CUs).
+// Below two full waves of 128-tiles the grid leaves CUs idle or unevenly loaded, so
+// the GEMM switches to 64-tiles (4x the tiles) and splits K until the grid has about
+// 1024 workgroups (2048 for SYRK, whose tiles are uniform), with at least 64 of K per
+// slice and ks*M*N within the caller's workspace.  Row/column epilogues keep 128
+// (their partial sums are laid out per 128-tile).  Thresholds from the
+// tools/gemm_bench.cpp sweep on MI355X (profiles/r1_gemm_sweep.txt): e.g. a
+// 1280-level triangular product 161 us -> 58 us, 2560-level 31 -> 47 TF/s.
+GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap) {
+  if (p.tile) return {p.tile, p.ksplit > 1 ? p.ksplit : 1};
+  if (epi != EPI_STORE || p.ksplit > 1) return {128, p.ksplit > 1 ? p.ksplit : 1};
+  if (tiles_for(p, 128) >= 1024) return {128, 1};
+  const int64_t t64 = tiles_for(p, 64);
+  const int64_t target = p.lower_out ? 2048 : 1024;
+  int ks = 1;
+  while (ks < 8 && t64 * ks < target && p.K / (2 * ks) >= 64 &&
+         (int64_t)(2 * ks) * p.M * p.N <= ws_cap)
+    ks *= 2;
+  return {64, ks};
+}
+
 hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipStream_t s) {
   GemmParams p = pin;
   if (p.M % GPS_TILE || p.N % GPS_TILE || p.K % BK || p.M <= 0 || p.N <= 0)
@@ -309,21 +354,33 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   if ((p.lda & 1) || (p.ldb & 1) || (p.ldc & 1)) return hipErrorInvalidValue;
   if (p.lower_out && p.M != p.N) return hipErrorInvalidValue;
   if (p.ksplit < 1) p.ksplit = 1;
-  if (p.ksplit > 1 && (epi != EPI_STORE || p.beta != 0.0)) return hipErrorInvalidValue;
-  // tile choice: 64×64 when a 128-tile grid would leave most of the 256 CUs idle
-  // (the bottom of the recursion); the row / column epilogue slabs are laid out
-  // per 128-tile, so those epilogues keep the 128 tile.
-  const int64_t t128 = p.lower_out ? (int64_t)(p.M / 128) * (p.M / 128 + 1) / 2
-                                   : (int64_t)(p.M / 128) * (p.N / 128);
-  const int tile = (epi == EPI_STORE && p.ksplit == 1 && t128 < 64) ? 64 : 128;
-  p.tiles_m = p.M / tile;
-  p.tiles_n = p.N / tile;
-  const int tiles = p.lower_out ? p.tiles_m * (p.tiles_m + 1) / 2 : p.tiles_m * p.tiles_n;
-  dim3 grid(tiles, p.ksplit), block(256);
+  const GemmPlan plan = gemm_plan(epi, p, p.ws ? p.ws_cap : 0);
+  const int tile = plan.tile;
+  if (tile != 64 && tile != 128) return hipErrorInvalidValue;
+  if (tile == 64 && epi != EPI_STORE) return hipErrorInvalidValue;
+  p.ksplit = plan.ksplit;
+  // split-K: with a workspace, slices go to slabs and an ordered reduction applies
+  // alpha/beta; without one (legacy FITC path) slice s writes C + s*c_kslice_stride
+  const bool slabbed = p.ksplit > 1 && p.ws != nullptr;
+  if (p.ksplit > 1 && !slabbed && (epi != EPI_STORE || p.beta != 0.0)) return hipErrorInvalidValue;
+  GemmParams q = p;
+  if (slabbed) {
+    if (epi != EPI_STORE) return hipErrorInvalidValue;
+    q.C = p.ws;
+    q.ldc = p.N;
+    q.c_kslice_stride = (int64_t)p.M * p.N;
+    q.alpha = 1.0;
+    q.beta = 0.0;
+  }
+  q.tiles_m = q.M / tile;
+  q.tiles_n = q.N / tile;
+  const int tiles = (int)tiles_for(q, tile);
+  dim3 grid(tiles, q.ksplit), block(256);
+  hipError_t err = hipErrorInvalidValue;
 #define GPS_GEMM_CASE(AL, BL, EP, T)                                               \
-  if (alay == AL && blay == BL && epi == EP && tile == T) {                        \
-    hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T>), grid, block, 0, s, p);    \
-    return hipGetLastError();                                                      \
+  if (err == hipErrorInvalidValue && alay == AL && blay == BL && epi == EP && tile == T) { \
+    hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T>), grid, block, 0, s, q);   \
+    err = hipGetLastError();                                                       \
   }
   GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE, 128)
   GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE, 128)
@@ -336,7 +393,11 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE, 64)
   GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE, 64)
 #undef GPS_GEMM_CASE
-  return hipErrorInvalidValue;
+  if (err != hipSuccess || !slabbed) return err;
+  const int64_t pairs = (int64_t)p.M * p.N / 2;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s,
+                     p.ws, p.ksplit, p.M, p.N, p.lower_out ? tile : 0, p.alpha, p.beta, p.C, p.ldc);
+  return hipGetLastError();
 }
 
 }  // namespace gps

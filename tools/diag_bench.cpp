@@ -1,19 +1,56 @@
-// Ablation timing of the 128×128 diagonal-block kernel (potrf + inverse).
-// Built four times with GPS_DIAG_ABLATE = 0..3 by tools/run_diag_bench.sh.
+// Timing + correctness of the 128×128 diagonal-block kernel (potrf + inverse).
+// tools/run_diag_bench.sh builds it for the production kernel (v3) and for -DGPS_DIAG_V1.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdio.h>
-#include <vector>
 #include <algorithm>
+#include <vector>
 #include "kernels_potrf.hip"
 using namespace gps;
 int main() {
   const int n = 128;
   std::vector<double> h(n * n);
   for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) h[i * n + j] = (i == j ? n : 0.0) + 1.0 / (1 + i + j);
-  double *A, *Li, *ld; int* info;
-  hipMalloc(&A, n * n * 8); hipMalloc(&Li, n * n * 8); hipMalloc(&ld, n * 8); hipMalloc(&info, 4);
+    for (int j = 0; j < n; ++j) h[i * n + j] = (i == j ? 4.0 : 0.0) + exp(-0.01 * (i - j) * (i - j)) + 1e-3 * ((i * 7 + j * 7) % 13);
+  // CPU reference: L (lower Cholesky) and L⁻¹
+  std::vector<double> L(n * n, 0.0), X(n * n, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double d = h[j * n + j];
+    for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+    L[j * n + j] = sqrt(d);
+    for (int i = j + 1; i < n; ++i) {
+      double s = h[i * n + j];
+      for (int k = 0; k < j; ++k) s -= L[i * n + k] * L[j * n + k];
+      L[i * n + j] = s / L[j * n + j];
+    }
+  }
+  for (int c = 0; c < n; ++c)
+    for (int r = c; r < n; ++r) {
+      double s = r == c ? 1.0 : 0.0;
+      for (int k = c; k < r; ++k) s -= L[r * n + k] * X[k * n + c];
+      X[r * n + c] = s / L[r * n + r];
+    }
+  double *A, *Li, *Lo, *ld; int* info;
+  hipMalloc(&A, n * n * 8); hipMalloc(&Li, n * n * 8); hipMalloc(&Lo, n * n * 8);
+  hipMalloc(&ld, n * 8); hipMalloc(&info, 4);
   hipMemcpy(A, h.data(), n * n * 8, hipMemcpyHostToDevice);
+  hipMemset(Li, 0x7f, n * n * 8); hipMemset(Lo, 0x7f, n * n * 8);
+  hipMemset(info, 0x7f, 4);
+  launch_potrf_diag(A, n, Li, n, Lo, n, ld, info, 0, n, 0);
+  std::vector<double> gLi(n * n), gLo(n * n), gld(n);
+  int ginfo;
+  hipMemcpy(gLi.data(), Li, n * n * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(gLo.data(), Lo, n * n * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(gld.data(), ld, n * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(&ginfo, info, 4, hipMemcpyDeviceToHost);
+  double eL = 0, eX = 0, eD = 0;
+  for (int i = 0; i < n * n; ++i) {
+    eL = std::max(eL, fabs(gLo[i] - L[i]));
+    eX = std::max(eX, fabs(gLi[i] - X[i]));
+  }
+  for (int i = 0; i < n; ++i) eD = std::max(eD, fabs(gld[i] - log(L[i * n + i])));
+  printf("max|dL| %.2e  max|dLinv| %.2e  max|dlog| %.2e  info %s\n", eL, eX, eD,
+         ginfo == 0x7f7f7f7f ? "untouched" : "SET");
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   for (int w = 0; w < 20; ++w) launch_potrf_diag(A, n, Li, n, nullptr, 0, ld, info, 0, n, 0);
   const int reps = 200;
@@ -21,26 +58,13 @@ int main() {
   for (int r = 0; r < reps; ++r) launch_potrf_diag(A, n, Li, n, nullptr, 0, ld, info, 0, n, 0);
   hipEventRecord(e1); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
-  printf("ablate=%d  %.2f us per diag block\n", GPS_DIAG_ABLATE, 1e3 * ms / reps);
-#ifdef GPS_DIAG_STAMPS
-  std::vector<unsigned long long> st(32 * 8 * 17);
-  hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(gps_stamps), st.size() * 8);
-  // per step: owner pivot (slot1-slot0 of the owner), barrier1 wait (max over waves of 2-1),
-  // panel (3-2), barrier2 (4-3), rest of step (next 0 - 4)
-  double sp = 0, sb1 = 0, spn = 0, sb2 = 0, st_ = 0;
-  for (int jb = 0; jb < 32; ++jb) {
-    auto S = [&](int slot, int w) { return (double)st[(jb * 8 + slot) * 17 + w]; };
-    double piv = S(1, 16) - S(0, 16);
-    double t0 = 1e30, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-    for (int w = 0; w < 16; ++w) { t0 = std::min(t0, S(0, w)); t1 = std::max(t1, S(1, w)); t2 = std::max(t2, S(2, w)); t3 = std::max(t3, S(3, w)); t4 = std::max(t4, S(4, w)); }
-    double next = jb < 31 ? 1e30 : t4;
-    if (jb < 31) for (int w = 0; w < 16; ++w) next = std::min(next, (double)st[((jb + 1) * 8 + 0) * 17 + w]);
-    if (jb < 4 || jb == 16 || jb == 30)
-      printf("jb=%2d pivot(owner)=%6.0f  t0->allarrive1=%6.0f  bar1->allarrive3=%6.0f  ->allarrive4=%6.0f  ->next=%6.0f\n",
-             jb, piv, t1 - t0, t3 - t2, t4 - t3, next - t4);
-    sp += piv; sb1 += t1 - t0; spn += t3 - t2; sb2 += t4 - t3; st_ += next - t4;
-  }
-  printf("sum cycles: pivot %.0f  phaseA %.0f  panel %.0f  bar2 %.0f  trailing %.0f\n", sp, sb1, spn, sb2, st_);
-#endif
-  return 0;
+  printf("%.2f us per diag block (no Lout)\n", 1e3 * ms / reps);
+  hipEventRecord(e0);
+  for (int r = 0; r < reps; ++r) launch_potrf_diag(A, n, Li, n, Lo, n, ld, info, 0, n, 0);
+  hipEventRecord(e1); hipEventSynchronize(e1);
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("%.2f us per diag block (with Lout)\n", 1e3 * ms / reps);
+  const bool ok = eL < 1e-12 && eX < 1e-12 && eD < 1e-13 && ginfo == 0x7f7f7f7f;
+  printf("%s\n", ok ? "PASS" : "FAIL");
+  return ok ? 0 : 1;
 }

@@ -30,7 +30,65 @@ static double run(int al, int bl, int epi, GemmParams p, int reps, double flops)
   return flops * reps / (ms * 1e-3) / 1e12;
 }
 
-int main() {
+// sweep: every recursion-level shape of the C3/C5 factorisation under each launch
+// plan (tile 128/64 x split-K 1/2/4/8), to fit gemm_plan's thresholds
+static int sweep(double* A, double* B, double* C, double* ws) {
+  struct S { const char* name; int M, N, K, al, bl, tri, lower; } cs[] = {
+    {"L5k tri1 NN", 5120, 4992, 5120, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L5k tri2 NT", 5120, 4992, 4992, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L5k tri3 NN", 5120, 4992, 4992, LAY_N, LAY_N, TRI_K_GE_J, 0},
+    {"L5k syrk", 5120, 5120, 4992, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L2.5k tri1 NN", 2560, 2432, 2560, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L2.5k tri2 NT", 2560, 2432, 2432, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L2.5k tri3 NN", 2560, 2432, 2432, LAY_N, LAY_N, TRI_K_GE_J, 0},
+    {"L2.5k syrk", 2560, 2560, 2432, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L2k tri1 NN", 2048, 2048, 2048, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L2k syrk", 2048, 2048, 2048, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L1280 tri1 NN", 1280, 1152, 1280, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L1280 tri2 NT", 1280, 1152, 1152, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L1280 tri3 NN", 1280, 1152, 1152, LAY_N, LAY_N, TRI_K_GE_J, 0},
+    {"L1280 syrk", 1280, 1280, 1152, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L1k tri1 NN", 1024, 1024, 1024, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L1k syrk", 1024, 1024, 1024, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L640 tri1 NN", 640, 640, 640, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L640 tri2 NT", 640, 640, 640, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L640 syrk", 640, 640, 640, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L384 tri1 NN", 384, 256, 384, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L384 syrk", 384, 384, 256, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L256 tri1 NN", 256, 128, 256, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L256 syrk", 256, 256, 128, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L128 tri1 NN", 128, 128, 128, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L128 tri2 NT", 128, 128, 128, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L128 syrk", 128, 128, 128, LAY_N, LAY_T, TRI_NONE, 1},
+  };
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (auto& c : cs) {
+    p.A = A; p.B = B; p.C = C; p.ws = ws;
+    p.lda = c.al == LAY_N ? c.K : c.M;
+    p.ldb = c.bl == LAY_T ? c.K : c.N;
+    p.ldc = c.N;
+    p.M = c.M; p.N = c.N; p.K = c.K; p.tri = c.tri; p.lower_out = c.lower;
+    p.alpha = c.lower ? -1.0 : 1.0; p.beta = c.lower ? 1.0 : 0.0;
+    const double fl = c.lower ? (double)c.M * (c.M + 1) * c.K : (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.K;
+    const int reps = fl > 1e11 ? 10 : (fl > 1e9 ? 100 : 400);
+    p.tile = 0; p.ksplit = 1;
+    const GemmPlan auto_plan = gemm_plan(EPI_STORE, p, 1ll << 40);
+    printf("%-16s auto(t%d,k%d) %7.2f |", c.name, auto_plan.tile, auto_plan.ksplit,
+           run(c.al, c.bl, EPI_STORE, p, reps, fl));
+    for (int tile : {128, 64})
+      for (int ks : {1, 2, 4, 8}) {
+        if (c.K / ks < 64) continue;
+        p.tile = tile; p.ksplit = ks;
+        const double t = run(c.al, c.bl, EPI_STORE, p, reps, fl);
+        const double us = fl / (t * 1e12) * 1e6;
+        printf(" t%d/k%d %6.2f (%6.1fus)", tile, ks, t, us);
+      }
+    printf("\n");
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
   const int64_t n = 20480;
   double *A, *B, *C, *o0, *o1, *w;
   hipMalloc(&A, n * n * 8); hipMalloc(&B, n * n * 8); hipMalloc(&C, n * n * 8);
@@ -43,6 +101,10 @@ int main() {
   }
   hipMemset(w, 0, n * 8);
   printf("operands: %s\n", zeros ? "zeros" : "uniform random [-0.5, 0.5)");
+  if (argc > 1 && !strcmp(argv[1], "sweep")) {
+    double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);
+    return sweep(A, B, C, ws);
+  }
   GemmParams p; memset(&p, 0, sizeof(p)); p.alpha = 1; p.ksplit = 1;
   struct { const char* name; int M, N, K, al, bl, epi, tri, lower, l2; } cs[] = {
     {"NT 8192^3", 8192, 8192, 8192, LAY_N, LAY_T, EPI_STORE, TRI_NONE, 0, 0},
