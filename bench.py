@@ -198,6 +198,10 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-fitc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lookahead", type=int, default=2,
+                    help="recursion depths with a split (lookahead) trailing update; 0 disables")
+    ap.add_argument("--reserve-cus", type=int, default=None,
+                    help="CUs kept free of the off-critical-path streams (library default 16)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
@@ -208,6 +212,9 @@ def main():
     ctl = Ctl(world)
     import gpscore
     ctx = gpscore.Context(0 if args.rehearse else local)
+    ctx.set_lookahead(args.lookahead)
+    if args.reserve_cus is not None:
+        ctx.set_reserved_cus(args.reserve_cus)
     gp = gpscore.GP(ctx=ctx)
 
     # ---------------- full GP (replicas) ----------------

@@ -62,8 +62,12 @@ int gps_ctx_synchronize(gps_ctx* ctx);
 
 /* ---- options ---------------------------------------------------------------- */
 enum {
-  GPS_OPT_OVERLAP = 0  /* 1 (default): off-critical-path GEMMs of the factorisation run on a
-                          second HIP stream; 0: everything on one stream (clean per-kernel timing) */
+  GPS_OPT_OVERLAP = 0,  /* 1 (default): off-critical-path GEMMs of the factorisation run on
+                           extra HIP streams; 0: everything on one stream (clean per-kernel timing) */
+  GPS_OPT_LOOKAHEAD = 1, /* recursion depths (0..2, default 2) whose trailing update is split so
+                           the child's leading block is factored while the rest is updated */
+  GPS_OPT_RESERVE_CUS = 2 /* CUs (default 16) the off-critical-path streams never use, so the
+                           latency-bound main-stream chain always finds free CUs */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -61,7 +61,11 @@ struct gps_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = true;
   hipStream_t side = nullptr;          // second stream for off-critical-path GEMMs
+  hipStream_t look[2] = {nullptr, nullptr};  // lookahead trailing updates, recursion depth 0 / 1
   bool overlap = true;                 // GPS_OPT_OVERLAP
+  int lookahead = 2;                   // GPS_OPT_LOOKAHEAD: recursion depths with a split update
+  int reserve_cus = 16;                // GPS_OPT_RESERVE_CUS: CUs kept free of off-path streams
+  int ncu = 0;
   std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
   size_t sync_used = 0;
   std::string err;
@@ -98,8 +102,8 @@ struct gps_ctx {
   int nranks = 1, rank = 0;
   // ---- compat scratch (gps_gram / potrf / potrs / diag_inv / scores)
   DBuf t0, t1, t2, t3, t4;
-  // ---- split-K slabs, one per stream (GEMMs on the two streams run concurrently)
-  DBuf ws_main, ws_side;
+  // ---- split-K slabs, one per stream (GEMMs on different streams run concurrently)
+  DBuf ws_main, ws_side, ws_look[2];
 };
 
 namespace {
@@ -227,7 +231,10 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
   if (!st) st = ctx->stream;
   GemmParams q = p;
   if (epi == EPI_STORE && q.ksplit == 1 && !q.ws) {  // let gemm_plan split K on small grids
-    DBuf& ws = st == ctx->side ? ctx->ws_side : ctx->ws_main;
+    DBuf& ws = st == ctx->side      ? ctx->ws_side
+               : st == ctx->look[0] ? ctx->ws_look[0]
+               : st == ctx->look[1] ? ctx->ws_look[1]
+                                    : ctx->ws_main;
     HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8));
     q.ws = ws.d();
     q.ws_cap = kSplitWsDoubles;
@@ -272,14 +279,23 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
 
 // recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
 // W is this level's workspace (n1·n2 doubles); deeper levels on the A22 side get
-// the region after it, so the side-stream GEMM that still reads this level's W
-// never races with them.  T = L21 L11⁻¹ only feeds the final L⁻¹21 product, so it
-// runs on ctx->side concurrently with the SYRK and rec(A22) (fork / join events).
+// the region after it, so a concurrent GEMM that still reads this level's W never
+// races with them.
+//
+// Streams (when ctx->overlap):
+//  * T = L21 L11⁻¹ only feeds the final L⁻¹21 product, so it runs off the main
+//    stream (fork / join events) concurrently with the trailing update and rec(A22);
+//  * lookahead (depth < ctx->lookahead): of the trailing update A22 -= W Wᵀ only the
+//    child's leading block B11 is on the main stream; B21 / B22 are updated on
+//    look[depth] while the child factors B11 (its latency-bound leaves leave most
+//    CUs idle).  The child waits for that update (`pending`) just before it reads
+//    its own A21.  T of a lookahead level queues behind the update on the same stream.
 int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
                   int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
-                  int64_t ldlo) {
+                  int64_t ldlo, int depth, hipEvent_t pending) {
   hipStream_t s = ctx->stream;
   if (nb == 1) {
+    if (pending) HIPCHK(hipStreamWaitEvent(s, pending, 0));
     Prof pr(ctx, "potrf_diag128", 2.0 * 128 * 128 * 128 / 3.0, 0);
     HIPCHK(launch_potrf_diag(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, s));
     return 0;
@@ -291,8 +307,10 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   double* Li21 = Linv + (int64_t)n1 * ldl;
   double* Li22 = Li21 + n1;
   int rc;
-  if ((rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo)))
+  if ((rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo,
+                          depth + 1, nullptr)))
     return rc;
+  if (pending) HIPCHK(hipStreamWaitEvent(s, pending, 0));  // parent's lookahead update of A21/A22
   {  // W = L21 = A21 · L11⁻ᵀ
     GemmParams p = gp0();
     p.A = A21; p.lda = lda; p.B = Linv; p.ldb = ldl; p.C = W; p.ldc = n1;
@@ -301,30 +319,52 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   }
   if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
                                     (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
-  // fork: T = L21 · L11⁻¹ → A21 on the side stream
-  hipStream_t ts = ctx->overlap ? ctx->side : s;
-  hipEvent_t fork = sync_event(ctx), join = sync_event(ctx);
+  const bool look = ctx->overlap && depth < ctx->lookahead && n2b >= 2;
+  hipStream_t ts = !ctx->overlap ? s : (look ? ctx->look[depth] : ctx->side);
+  hipEvent_t fork = sync_event(ctx), join = sync_event(ctx), upd = nullptr;
   if (!fork || !join) return fail(ctx, -2, "hipEventCreate failed");
   if (ctx->overlap) {
     HIPCHK(hipEventRecord(fork, s));
     HIPCHK(hipStreamWaitEvent(ts, fork, 0));
   }
+  // trailing update A22 -= L21 L21ᵀ (lower tiles); with lookahead split at the child's
+  // split point m1: B11 on the main stream, B21 and B22 on ts
+  const int m1 = look ? (n2b / 2) * GPS_TILE : n2;
   {
+    GemmParams p = gp0();
+    p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
+    p.M = m1; p.N = m1; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
+  }
+  if (look) {
+    const int m2 = n2 - m1;
+    const double* W2 = W + (int64_t)m1 * n1;
+    {  // B21 -= W2 W1ᵀ
+      GemmParams p = gp0();
+      p.A = W2; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22 + (int64_t)m1 * lda; p.ldc = lda;
+      p.M = m2; p.N = m1; p.K = n1; p.alpha = -1.0; p.beta = 1.0;
+      if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p, ts))) return rc;
+    }
+    {  // B22 -= W2 W2ᵀ
+      GemmParams p = gp0();
+      p.A = W2; p.lda = n1; p.B = W2; p.ldb = n1; p.C = A22 + (int64_t)m1 * lda + m1; p.ldc = lda;
+      p.M = m2; p.N = m2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
+      if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p, ts))) return rc;
+    }
+    upd = sync_event(ctx);
+    if (!upd) return fail(ctx, -2, "hipEventCreate failed");
+    HIPCHK(hipEventRecord(upd, ts));
+  }
+  {  // T = L21 · L11⁻¹ → A21 (off the critical path)
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = Linv; p.ldb = ldl; p.C = A21; p.ldc = lda;
     p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
     if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, ts))) return rc;
   }
   if (ctx->overlap) HIPCHK(hipEventRecord(join, ts));
-  {  // A22 -= L21 L21ᵀ  (lower tiles)
-    GemmParams p = gp0();
-    p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
-    p.M = n2; p.N = n2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
-    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
-  }
   if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W + (int64_t)n1 * n2, n2b, logdiag + n1, info,
                           base + n1, nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr,
-                          ldlo)))
+                          ldlo, depth + 1, upd)))
     return rc;
   if (ctx->overlap) HIPCHK(hipStreamWaitEvent(s, join, 0));
   {  // L⁻¹21 = −L22⁻¹ · T
@@ -358,7 +398,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
               int nreal, double* Lout) {
   ctx->sync_used = 0;
   int rc = potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
-                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad);
+                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad, 0, nullptr);
   return rc;
 }
 
@@ -422,6 +462,32 @@ extern "C" {
 
 int gps_version(void) { return 100; }
 
+// (re)create the off-critical-path streams (side, look[]) with a CU mask that leaves
+// reserve_cus CUs, spread evenly over the device, to the main stream: a concurrent
+// big GEMM holds every workgroup slot with ~1 ms tiles, which would otherwise stall the
+// main stream's latency-bound chain (diag-block kernels need a whole CU's LDS).
+int make_aux_streams(gps_ctx* ctx) {
+  HIPCHK(hipDeviceSynchronize());
+  if (ctx->side) HIPCHK(hipStreamDestroy(ctx->side));
+  for (hipStream_t& l : ctx->look)
+    if (l) HIPCHK(hipStreamDestroy(l));
+  ctx->side = nullptr;
+  ctx->look[0] = ctx->look[1] = nullptr;
+  const int ncu = ctx->ncu, r = std::min(ctx->reserve_cus, ncu / 2);
+  std::vector<hipStream_t*> aux = {&ctx->side, &ctx->look[0], &ctx->look[1]};
+  if (r <= 0) {
+    for (hipStream_t* a : aux) HIPCHK(hipStreamCreateWithFlags(a, hipStreamNonBlocking));
+    return 0;
+  }
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  const int stride = ncu / r;
+  for (int i = 0; i < ncu; ++i)
+    if (!(i % stride == stride - 1 && i / stride < r)) mask[i / 32] |= 1u << (i % 32);
+  for (hipStream_t* a : aux)
+    HIPCHK(hipExtStreamCreateWithCUMask(a, (uint32_t)mask.size(), mask.data()));
+  return 0;
+}
+
 int gps_ctx_create(int device, gps_ctx** out) {
   gps_ctx* ctx = nullptr;
   if (!out) return fail(nullptr, -1, "out is NULL");
@@ -434,7 +500,8 @@ int gps_ctx_create(int device, gps_ctx** out) {
   ctx->device = device;
   HIPCHK(hipSetDevice(device));
   HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  HIPCHK(hipDeviceGetAttribute(&ctx->ncu, hipDeviceAttributeMultiprocessorCount, device));
+  if (int rc = make_aux_streams(ctx)) return rc;
   HIPCHK(hipHostMalloc((void**)&ctx->hsmall, 256 * sizeof(double), hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&ctx->hinfo, 16, hipHostMallocDefault));
   HIPCHK(ensure(ctx->info, 16));
@@ -456,11 +523,13 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
                  &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
-                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side};
+                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_look[0], &ctx->ws_look[1]};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  for (hipStream_t l : ctx->look)
+    if (l) (void)hipStreamDestroy(l);
   if (ctx->hsmall) (void)hipHostFree(ctx->hsmall);
   if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -488,6 +557,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
   if (int rc = bind(ctx)) return rc;
   switch (key) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
+    case GPS_OPT_LOOKAHEAD: ctx->lookahead = value < 0 ? 0 : (value > 2 ? 2 : value); return 0;
+    case GPS_OPT_RESERVE_CUS:
+      ctx->reserve_cus = value < 0 ? 0 : value;
+      return make_aux_streams(ctx);
     default: return fail(ctx, -1, "unknown option");
   }
 }

@@ -54,15 +54,38 @@ constexpr int GROUP_M = 8;
 // 35-45 TF/s, plain grouped order 64.6, heaviest-first 68.9.  Workgroups are
 // dealt to XCDs in block order, so an XCD whose slots are all held by long tiles
 // stalls the dispatch of every later block; equal-work neighbours in block order
-// (which land on different XCDs) avoid that.
-__device__ __forceinline__ void tile_of(const GemmParams& p, int t, int& ti, int& tj) {
+// (which land on different XCDs) avoid that.  Map 3 (the default for triangular
+// operands since the microbenchmark below) keeps that equal-work-per-XCD property
+// but gives each XCD a compact band of tiles: 70.7 TF/s on the same TRMM.
+__device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int& tj) {
   if (p.lower_out) {
     int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
     while ((r + 1) * (r + 2) / 2 <= t) ++r;
     while (r * (r + 1) / 2 > t) --r;
     ti = r;
     tj = t - r * (r + 1) / 2;
-    return;
+    return true;
+  }
+  if (p.map_mode == 3) {
+    // XCD-banded heaviest-first (triangular operands): block b runs on XCD b % 8;
+    // XCD x owns a contiguous band of the index that does NOT carry the triangular
+    // work and walks the other index heaviest-first, so every XCD gets the same work
+    // profile (balanced under in-order dispatch) while its ~64 resident tiles form a
+    // compact 2-D patch (both operand panels reused from its own L2).  Positions past
+    // the matrix edge are holes (the workgroup exits at once).
+    const int x = t & 7, i = t >> 3;
+    if (p.tri == TRI_K_LE_I || p.tri == TRI_K_GE_I) {  // work grows/shrinks with ti
+      const int bw = (p.tiles_n + 7) >> 3;
+      const int ri = i / bw;
+      tj = x * bw + i % bw;
+      ti = p.tri == TRI_K_LE_I ? p.tiles_m - 1 - ri : ri;
+      return tj < p.tiles_n && ri < p.tiles_m;
+    }
+    const int bh = (p.tiles_m + 7) >> 3;  // TRI_K_LE_J / TRI_K_GE_J: work follows tj
+    const int cj = i / bh;
+    ti = x * bh + i % bh;
+    tj = p.tri == TRI_K_LE_J ? p.tiles_n - 1 - cj : cj;
+    return ti < p.tiles_m && cj < p.tiles_n;
   }
   const int per_group = GROUP_M * p.tiles_n;
   const int g = t / per_group;
@@ -71,10 +94,11 @@ __device__ __forceinline__ void tile_of(const GemmParams& p, int t, int& ti, int
   const int tt = t - g * per_group;
   ti = first + tt % gm;
   tj = tt / gm;
-  if (p.map_mode != 0) return;
+  if (p.map_mode != 0) return true;
   if (p.tri == TRI_K_LE_I) ti = p.tiles_m - 1 - ti;       // K grows with ti
   else if (p.tri == TRI_K_LE_J) tj = p.tiles_n - 1 - tj;  // K grows with tj
   // TRI_K_GE_I / TRI_K_GE_J: K shrinks with the index, natural order is heaviest-first
+  return true;
 }
 
 // bijective XCD-contiguous remap: blocks b, b+8, b+16, ... (one XCD under the
@@ -103,7 +127,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   int ti, tj;
   const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
   // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
-  tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj);
+  if (!tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj)) return;
   const int row0 = ti * TILE, col0 = tj * TILE;
 
   int kb = 0, ke = p.K;
@@ -374,7 +398,15 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   }
   q.tiles_m = q.M / tile;
   q.tiles_n = q.N / tile;
-  const int tiles = (int)tiles_for(q, tile);
+  int tiles = (int)tiles_for(q, tile);
+  // triangular operands default to the XCD-banded heaviest-first order (map 3):
+  // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build
+  if (q.map_mode == 0 && q.tri != TRI_NONE && !q.lower_out) q.map_mode = 3;
+  if (q.map_mode == 3) {
+    if (q.lower_out || q.tri == TRI_NONE) return hipErrorInvalidValue;
+    tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
+                                                          : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;
+  }
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
 #define GPS_GEMM_CASE(AL, BL, EP, T)                                               \

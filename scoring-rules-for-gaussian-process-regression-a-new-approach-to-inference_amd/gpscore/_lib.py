@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
-GPS_OPT_OVERLAP = 0
+GPS_OPT_OVERLAP, GPS_OPT_LOOKAHEAD, GPS_OPT_RESERVE_CUS = 0, 1, 2
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
@@ -155,6 +155,14 @@ class Context:
     def set_overlap(self, on=True):
         """Run the factorisation's off-critical-path GEMMs on a second stream."""
         self.call("gps_ctx_set_option", GPS_OPT_OVERLAP, 1 if on else 0)
+
+    def set_lookahead(self, depth=2):
+        """Recursion depths whose trailing update is split for lookahead (0 disables)."""
+        self.call("gps_ctx_set_option", GPS_OPT_LOOKAHEAD, int(depth))
+
+    def set_reserved_cus(self, n=16):
+        """CUs the off-critical-path streams may not use (recreates those streams)."""
+        self.call("gps_ctx_set_option", GPS_OPT_RESERVE_CUS, int(n))
 
     def synchronize(self):
         self.call("gps_ctx_synchronize")

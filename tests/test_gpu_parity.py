@@ -114,6 +114,34 @@ def test_full_gp_large_properties(gp):
     assert abs(o["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
+def test_stream_schedules_agree(gp, gpu_ctx):
+    """Lookahead (split trailing update on extra streams), side-stream overlap and the
+    single-stream schedule compute the same factorisation: only the split-K plan of
+    the split updates may change the summation grouping, so agreement is ~1e-13."""
+    rng = np.random.default_rng(11)
+    n, nt, d = 6016, 512, 8
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
+    y, yt = np.sin(X.sum(1)), np.sin(Xt.sum(1))
+    th = (0.0, np.log(1.5) * np.ones(d), np.log(0.01))
+    runs = []
+    for overlap, look in ((True, 2), (True, 0), (False, 0)):
+        gpu_ctx.set_overlap(overlap)
+        gpu_ctx.set_lookahead(look)
+        r = gp.fit(X, y, th)
+        mu, var = gp.predict(Xt, yt)
+        runs.append((r, mu, var))
+    gpu_ctx.set_overlap(True)
+    gpu_ctx.set_lookahead(2)
+    r0, mu0, var0 = runs[0]
+    for r, mu, var in runs[1:]:
+        assert nrel(r.mu_loo, r0.mu_loo) < 1e-11 and nrel(r.var_loo, r0.var_loo) < 1e-11
+        assert nrel(mu, mu0) < 1e-11 and nrel(var, var0) < 1e-11
+        for k in ("nlml", "loo_crps", "loo_logs", "logdet"):
+            assert abs(r.objectives[k] - r0.objectives[k]) <= 1e-11 * max(1.0, abs(r0.objectives[k]))
+    f = O.fast_full_fit(X, y, *th)
+    assert nrel(r0.mu_loo, f["loo_mu"]) < 1e-9 and abs(r0.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
+
+
 def test_not_positive_definite_raises(gp):
     """torch.potrf raises RuntimeError on a non-PD leading minor (caught at KF:726);
     the C-ABI returns that minor's order as info > 0."""
