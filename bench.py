@@ -198,7 +198,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-fitc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--lookahead", type=int, default=2,
+    ap.add_argument("--lookahead", type=int, default=0,
                     help="recursion depths with a split (lookahead) trailing update; 0 disables")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs kept free of the off-critical-path streams (library default 16)")

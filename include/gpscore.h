@@ -64,10 +64,11 @@ int gps_ctx_synchronize(gps_ctx* ctx);
 enum {
   GPS_OPT_OVERLAP = 0,  /* 1 (default): off-critical-path GEMMs of the factorisation run on
                            extra HIP streams; 0: everything on one stream (clean per-kernel timing) */
-  GPS_OPT_LOOKAHEAD = 1, /* recursion depths (0..2, default 2) whose trailing update is split so
+  GPS_OPT_LOOKAHEAD = 1, /* recursion depths (0..2, default 0) whose trailing update is split so
                            the child's leading block is factored while the rest is updated */
-  GPS_OPT_RESERVE_CUS = 2 /* CUs (default 16) the off-critical-path streams never use, so the
-                           latency-bound main-stream chain always finds free CUs */
+  GPS_OPT_RESERVE_CUS = 2, /* CUs (default 0) the off-critical-path streams may not use (CU-masked
+                           streams; measured slower on MI355X, kept for experiments) */
+  GPS_OPT_GEMM_MAP = 3    /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -63,8 +63,10 @@ struct gps_ctx {
   hipStream_t side = nullptr;          // second stream for off-critical-path GEMMs
   hipStream_t look[2] = {nullptr, nullptr};  // lookahead trailing updates, recursion depth 0 / 1
   bool overlap = true;                 // GPS_OPT_OVERLAP
-  int lookahead = 2;                   // GPS_OPT_LOOKAHEAD: recursion depths with a split update
-  int reserve_cus = 16;                // GPS_OPT_RESERVE_CUS: CUs kept free of off-path streams
+  int lookahead = 0;                   // GPS_OPT_LOOKAHEAD: recursion depths with a split update
+                                       // (measured neutral on C3: 131.2 vs 130.1 ms; off by default)
+  int reserve_cus = 0;                 // GPS_OPT_RESERVE_CUS: CUs kept free of off-path streams
+  int gemm_map = 0;                    // GPS_OPT_GEMM_MAP: tile-order override (A/B measurements)
   int ncu = 0;
   std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
   size_t sync_used = 0;
@@ -230,6 +232,7 @@ double gemm_flops(const GemmParams& p) {
 int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t st = nullptr) {
   if (!st) st = ctx->stream;
   GemmParams q = p;
+  if (q.map_mode == 0) q.map_mode = ctx->gemm_map;
   if (epi == EPI_STORE && q.ksplit == 1 && !q.ws) {  // let gemm_plan split K on small grids
     DBuf& ws = st == ctx->side      ? ctx->ws_side
                : st == ctx->look[0] ? ctx->ws_look[0]
@@ -479,10 +482,11 @@ int make_aux_streams(gps_ctx* ctx) {
     for (hipStream_t* a : aux) HIPCHK(hipStreamCreateWithFlags(a, hipStreamNonBlocking));
     return 0;
   }
+  // CU ids interleave over the XCDs (id % 8 on MI355X: a stride-16 mask that removed
+  // one XCD's CUs halved the masked streams' throughput under in-order dispatch), so the
+  // top r ids take r/8 CUs from every XCD
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  const int stride = ncu / r;
-  for (int i = 0; i < ncu; ++i)
-    if (!(i % stride == stride - 1 && i / stride < r)) mask[i / 32] |= 1u << (i % 32);
+  for (int i = 0; i < ncu - r; ++i) mask[i / 32] |= 1u << (i % 32);
   for (hipStream_t* a : aux)
     HIPCHK(hipExtStreamCreateWithCUMask(a, (uint32_t)mask.size(), mask.data()));
   return 0;
@@ -558,6 +562,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
   switch (key) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
     case GPS_OPT_LOOKAHEAD: ctx->lookahead = value < 0 ? 0 : (value > 2 ? 2 : value); return 0;
+    case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
     case GPS_OPT_RESERVE_CUS:
       ctx->reserve_cus = value < 0 ? 0 : value;
       return make_aux_streams(ctx);
@@ -995,9 +1000,17 @@ int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_
   HIPCHK(ensure(ctx->tvec, mp * 8));
   const int64_t red_len = mp * mp + mp + 8;
   HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
-  // split-K for the m×m SYRK over n rows: aim at ~2048 workgroups
+  // split-K for the m×m SYRK over n rows.  Every workgroup has the same work, so the
+  // grid runs in whole rounds of 512 slots (2 per CU): take the smallest split whose last
+  // round is >= 95 % full (528 tiles at m = 4096: ks 3 -> 77 % of the slots busy on
+  // average, ks 12 -> 95 %), with at least 1024 rows per slice and at most 32 slabs.
   const int64_t tiles_lower = tm * (tm + 1) / 2;
-  int ks = (int)std::max<int64_t>(1, std::min<int64_t>(np / GPS_TILE, 2048 / tiles_lower));
+  int ks = 1;
+  for (int k = 1; k <= 32 && (int64_t)k * 1024 <= np; ++k) {
+    const int64_t wg = tiles_lower * k, rounds = (wg + 511) / 512;
+    ks = k;
+    if (wg >= 1024 && (double)wg / (512.0 * rounds) >= 0.95) break;
+  }
   HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
   const int64_t nchunk = (std::max(np, mp) + 255) / 256;
   const int64_t fslab_len = std::max<int64_t>(tm * np, nchunk * mp * 2);

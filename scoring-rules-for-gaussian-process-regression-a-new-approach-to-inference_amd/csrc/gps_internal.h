@@ -57,7 +57,8 @@ struct GemmParams {
   int ksplit;                // number of K slices (grid.y)
   int tri;
   int tiles_m, tiles_n;
-  int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap
+  int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
+                             // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)

@@ -402,6 +402,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // triangular operands default to the XCD-banded heaviest-first order (map 3):
   // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build
   if (q.map_mode == 0 && q.tri != TRI_NONE && !q.lower_out) q.map_mode = 3;
+  else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
   if (q.map_mode == 3) {
     if (q.lower_out || q.tri == TRI_NONE) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m

@@ -37,6 +37,9 @@ __device__ __forceinline__ void lds_read4(const double* p, double (&v)[4]) {
 #ifdef GPS_DIAG_STAMPS
 __device__ unsigned long long gps_stamps[32 * 8 * 17];
 #endif
+#ifdef GPS_V3_STAMPS
+__device__ unsigned long long gps_stamps3[32 * 8];
+#endif
 
 __global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restrict__ A, int64_t lda,
                                                           double* __restrict__ Linv, int64_t ldl,
@@ -323,9 +326,22 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
 #ifndef GPS_V3_ABLATE
 #define GPS_V3_ABLATE 0  // tools/diag_bench.cpp: 1 no inverse, 2 no trailing update, 4 no factor loop
 #endif
+#ifdef GPS_V3_STAMPS  // tools/diag_bench.cpp: per-phase s_memtime of the wave owning column jb
+#define S3(slot)                                                                        \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long _t;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    if (lane == 0) gps_stamps3[jb * 8 + (slot)] = _t;                                   \
+  } while (0)
+#else
+#define S3(slot) do {} while (0)
+#endif
   // ======================= factorisation =======================
   for (int jb = 0; jb < ((GPS_V3_ABLATE & 4) ? 0 : 32); ++jb) {
     const bool mine = w == wave_of_col(jb);  // wave-uniform
+    if (mine) S3(0);
     if (mine) __builtin_amdgcn_s_setprio(2);
     if (jb > 0 && active && bc >= jb && !(GPS_V3_ABLATE & 2)) {  // a. rank-4 update, L column jb-1
       const double* cb = CB + ((jb - 1) & 1) * 4 * NB;
@@ -346,6 +362,7 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
         }
     }
     if (mine) {  // b. pivot (redundantly in every lane of this wave) + panel
+      S3(1);
       int ljj = 0;
       for (int c = cs; c < jb; ++c) ljj += 32 - c;
       ljj = __builtin_amdgcn_readfirstlane(ljj);
@@ -386,9 +403,10 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
             x[r][c] = -t * is[r];
           }
         }
+      S3(2);
       double* cb = CB + (jb & 1) * 4 * NB;
-      if (active && bc == jb && br > jb) {
-        double L[4][4];  // L_rj = A_rj D⁻ᵀ: L[r][c] = Σ_{k<=c} a[r][k] x[c][k]
+      if (active && bc == jb && br > jb) {  // panel: L_rj = A_rj D⁻ᵀ, kept in a[][]
+        double L[4][4];                     // L[r][c] = Σ_{k<=c} a[r][k] x[c][k]
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -399,54 +417,86 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
             L[r][c] = s;
           }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {  // publish the panel first (critical path)
+        for (int c = 0; c < 4; ++c) {
           *reinterpret_cast<double2*>(&cb[c * NB + r0]) = make_double2(L[0][c], L[1][c]);
           *reinterpret_cast<double2*>(&cb[c * NB + r0 + 2]) = make_double2(L[2][c], L[3][c]);
         }
-        // P_rj = L_rj D⁻¹: P[r][c] = Σ_{k>=c} L[r][k] x[k][c]
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double p[4];
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            double s = 0.0;
-#pragma unroll
-            for (int k = c; k < 4; ++k) s = fma(L[r][k], x[k][c], s);
-            p[r] = s;
-          }
-          *reinterpret_cast<double2*>(&PT[(c0 + c) * LTS + r0]) = make_double2(p[0], p[1]);
-          *reinterpret_cast<double2*>(&PT[(c0 + c) * LTS + r0 + 2]) = make_double2(p[2], p[3]);
-        }
-        if (Lout) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            double2* dst = reinterpret_cast<double2*>(Lout + (int64_t)(r0 + r) * ldlo + c0);
-            dst[0] = make_double2(L[r][0], L[r][1]);
-            dst[1] = make_double2(L[r][2], L[r][3]);
-          }
-        }
+          for (int c = 0; c < 4; ++c) a[r][c] = L[r][c];
       }
-      if (lane == ljj) {  // the diagonal block's own lane
+      S3(3);
+      if (lane == ljj) {  // the diagonal block's own lane keeps L_jj (D⁻¹ is rebuilt after the loop)
         if (bad) atomicMin(info, base + bad);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          DG[4 * jb + r] = l[r][r];
-          *reinterpret_cast<double2*>(&DI[jb * 16 + r * 4]) = make_double2(x[r][0], x[r][1]);
-          *reinterpret_cast<double2*>(&DI[jb * 16 + r * 4 + 2]) = make_double2(x[r][2], x[r][3]);
-        }
-        if (Lout) {
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            double2* dst = reinterpret_cast<double2*>(Lout + (int64_t)(r0 + r) * ldlo + c0);
-            dst[0] = make_double2(l[r][0], r >= 1 ? l[r][1] : 0.0);
-            dst[1] = make_double2(r >= 2 ? l[r][2] : 0.0, r >= 3 ? l[r][3] : 0.0);
-          }
-        }
+          for (int c = 0; c < 4; ++c) a[r][c] = c <= r ? l[r][c] : 0.0;
       }
+      S3(4);
+      S3(5);
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
+    if (mine) S3(6);
   }
+  // ---- off the per-step critical path: D⁻¹ and L_jj of every diagonal block (in parallel)
+  if (active && br == bc) {
+    double x[4][4];  // x = L_jj⁻¹ (lower): x_cc = 1/L_cc, x_rc = -(1/L_rr) Σ_{c<=k<r} L_rk x_kc
+    double is[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) is[r] = 1.0 / a[r][r];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r < c) {
+          x[r][c] = 0.0;
+        } else if (r == c) {
+          x[r][c] = is[r];
+        } else {
+          double t = 0.0;
+#pragma unroll
+          for (int k = c; k < r; ++k) t = fma(a[r][k], x[k][c], t);
+          x[r][c] = -t * is[r];
+        }
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      DG[r0 + r] = a[r][r];
+      *reinterpret_cast<double2*>(&DI[br * 16 + r * 4]) = make_double2(x[r][0], x[r][1]);
+      *reinterpret_cast<double2*>(&DI[br * 16 + r * 4 + 2]) = make_double2(x[r][2], x[r][3]);
+    }
+  }
+  if (Lout && active) {  // L (diagonal blocks hold zeros above their diagonal)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double2* dst = reinterpret_cast<double2*>(Lout + (int64_t)(r0 + r) * ldlo + c0);
+      dst[0] = make_double2(a[r][0], a[r][1]);
+      dst[1] = make_double2(a[r][2], a[r][3]);
+    }
+  }
+  __syncthreads();
+  if (active && br > bc) {  // P_rb = L_rb D_b⁻¹ for the inverse: P[r][c] = Σ_{k>=c} L[r][k] x[k][c]
+    double di[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lds_read4(&DI[bc * 16 + r * 4], di[r]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double p[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = c; k < 4; ++k) s = fma(a[r][k], di[k][c], s);
+        p[r] = s;
+      }
+      *reinterpret_cast<double2*>(&PT[(c0 + c) * LTS + r0]) = make_double2(p[0], p[1]);
+      *reinterpret_cast<double2*>(&PT[(c0 + c) * LTS + r0 + 2]) = make_double2(p[2], p[3]);
+    }
+  }
+  __syncthreads();
   if (tid < NB) logdiag[tid] = log(DG[tid]);
   if (Lout) {  // zero blocks strictly above the block diagonal
     for (int e = tid; e < NB * 32; e += 64 * V3_WAVES) {

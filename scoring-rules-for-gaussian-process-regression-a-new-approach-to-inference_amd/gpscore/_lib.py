@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
-GPS_OPT_OVERLAP, GPS_OPT_LOOKAHEAD, GPS_OPT_RESERVE_CUS = 0, 1, 2
+GPS_OPT_OVERLAP, GPS_OPT_LOOKAHEAD, GPS_OPT_RESERVE_CUS, GPS_OPT_GEMM_MAP = 0, 1, 2, 3
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
@@ -156,7 +156,7 @@ class Context:
         """Run the factorisation's off-critical-path GEMMs on a second stream."""
         self.call("gps_ctx_set_option", GPS_OPT_OVERLAP, 1 if on else 0)
 
-    def set_lookahead(self, depth=2):
+    def set_lookahead(self, depth=0):
         """Recursion depths whose trailing update is split for lookahead (0 disables)."""
         self.call("gps_ctx_set_option", GPS_OPT_LOOKAHEAD, int(depth))
 

@@ -1,0 +1,74 @@
+"""Same-box A/B of library schedule options on a bench workload (MI355X boxes differ by
+~5% in GEMM clocks, so variants must be compared inside one run).
+
+  python tools/ab_bench.py --config C3 la=2,map=0 la=0,map=0 la=2,map=4
+  options: la (GPS_OPT_LOOKAHEAD), map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP)
+Variants are interleaved round-robin for --rounds rounds; prints the median ms/unit.
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd"))
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import gpscore  # noqa: E402
+from gpscore import _lib  # noqa: E402
+
+KEYS = {"la": _lib.GPS_OPT_LOOKAHEAD, "map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("variants", nargs="+")
+    args = ap.parse_args()
+    c = bench.CONFIGS[args.config]
+    ctx = gpscore.Context(0)
+    gp = gpscore.GP(ctx=ctx)
+    X, y, Xt, yt, Z, th = bench.synth(c["n"], c["d"], c["nt"], c["seed"], c.get("m"))
+    if Z is None:
+        gp.set_data(X, y)
+    else:
+        gp.set_data(X, y, kind="fitc", Z=Z)
+    gp.set_test(Xt, yt)
+
+    def unit():
+        gp.fit(theta=th, return_loo=False)
+        gp.predict(with_scores=True)
+
+    variants = []
+    for v in args.variants:
+        opts = {}
+        for kv in v.split(","):
+            k, val = kv.split("=")
+            opts[KEYS[k]] = int(val)
+        variants.append((v, opts))
+    unit()
+    times = {v: [] for v, _ in variants}
+    for _ in range(args.rounds):
+        for name, opts in variants:
+            for key, val in opts.items():
+                ctx.call("gps_ctx_set_option", key, val)
+            unit()
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                unit()
+            ctx.synchronize()
+            times[name].append(1e3 * (time.perf_counter() - t0) / args.steps)
+    for name, _ in variants:
+        ts = times[name]
+        print("%-24s median %8.2f ms/unit  (all: %s)" % (name, float(np.median(ts)),
+                                                        " ".join("%.2f" % t for t in ts)))
+
+
+if __name__ == "__main__":
+    main()

@@ -64,6 +64,26 @@ int main() {
   hipEventRecord(e1); hipEventSynchronize(e1);
   hipEventElapsedTime(&ms, e0, e1);
   printf("%.2f us per diag block (with Lout)\n", 1e3 * ms / reps);
+#ifdef GPS_V3_STAMPS
+  {
+    std::vector<unsigned long long> st(32 * 8);
+    hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(gps_stamps3), st.size() * 8);
+    double sum[7] = {0};
+    const char* nm[7] = {"update", "pivot", "panelL+CB", "P+PT", "DI/DG", "barrier", "->next"};
+    for (int jb = 0; jb < 32; ++jb) {
+      double d[7];
+      for (int k = 0; k < 6; ++k) d[k] = (double)(st[jb * 8 + k + 1] - st[jb * 8 + k]);
+      d[6] = jb < 31 ? (double)(st[(jb + 1) * 8] - st[jb * 8 + 6]) : 0.0;
+      for (int k = 0; k < 7; ++k) sum[k] += d[k];
+      if (jb < 3 || jb == 15 || jb == 30)
+        printf("jb=%2d upd %5.0f piv %5.0f L %5.0f P %5.0f DI %5.0f bar %5.0f next %5.0f\n", jb,
+               d[0], d[1], d[2], d[3], d[4], d[5], d[6]);
+    }
+    printf("sums:");
+    for (int k = 0; k < 7; ++k) printf(" %s %.0f", nm[k], sum[k]);
+    printf("\n");
+  }
+#endif
   const bool ok = eL < 1e-12 && eX < 1e-12 && eD < 1e-13 && ginfo == 0x7f7f7f7f;
   printf("%s\n", ok ? "PASS" : "FAIL");
   return ok ? 0 : 1;
