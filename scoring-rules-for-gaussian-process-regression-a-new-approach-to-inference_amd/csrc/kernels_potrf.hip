@@ -372,11 +372,9 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
 #pragma unroll
         for (int c = 0; c <= r; ++c) l[r][c] = readlane_f64(a[r][c], ljj);
       double is[4];
-      int bad = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const double d = l[j][j];
-        if (!(d > 0.0) && bad == 0 && 4 * jb + j < nreal) bad = 4 * jb + j + 1;
+        const double d = l[j][j];  // d <= 0 or NaN leaves L_jj = d*rsqrt(d) NaN: checked after the loop
         is[j] = rsqrt(d);
         l[j][j] = d * is[j];
 #pragma unroll
@@ -428,7 +426,6 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
       }
       S3(3);
       if (lane == ljj) {  // the diagonal block's own lane keeps L_jj (D⁻¹ is rebuilt after the loop)
-        if (bad) atomicMin(info, base + bad);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -443,6 +440,13 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
   }
   // ---- off the per-step critical path: D⁻¹ and L_jj of every diagonal block (in parallel)
   if (active && br == bc) {
+    // first non-positive pivot (torch.potrf's leading-minor index): a bad pivot makes its
+    // L_ii NaN and poisons every later one, so the minimum flagged index is the first
+    int bad = 0;
+#pragma unroll
+    for (int r = 3; r >= 0; --r)
+      if (!(a[r][r] > 0.0) && r0 + r < nreal) bad = r0 + r + 1;
+    if (bad) atomicMin(info, base + bad);
     double x[4][4];  // x = L_jj⁻¹ (lower): x_cc = 1/L_cc, x_rc = -(1/L_rr) Σ_{c<=k<r} L_rk x_kc
     double is[4];
 #pragma unroll

@@ -88,6 +88,34 @@ static int sweep(double* A, double* B, double* C, double* ws) {
   return 0;
 }
 
+// leading-dimension study: the 10k-level shapes of the C3 build with the operands'
+// real leading dimension (n_pad = 20096) against compact and padded alternatives
+static int ldstudy(double* A, double* B, double* C) {
+  struct S { const char* name; int M, N, K, al, bl, tri, lower; } cs[] = {
+    {"K_LE_I NN 10112x9984x10112", 10112, 9984, 10112, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"K_LE_J NT 10112x9984x9984", 10112, 9984, 9984, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"K_GE_J NN 10112x9984x9984", 10112, 9984, 9984, LAY_N, LAY_N, TRI_K_GE_J, 0},
+    {"SYRK NT 10112 K=9984", 10112, 10112, 9984, LAY_N, LAY_T, TRI_NONE, 1},
+    {"TRMM-colred 20096x5120", 20096, 5120, 20096, LAY_N, LAY_T, TRI_K_LE_I, 0},
+  };
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (auto& c : cs) {
+    for (int64_t ld : {0l, 20096l, 20160l, 20480l, 20608l}) {
+      p.A = A; p.B = B; p.C = C;
+      const int64_t lda0 = c.al == LAY_N ? c.K : c.M, ldb0 = c.bl == LAY_T ? c.K : c.N;
+      p.lda = ld ? ld : lda0; p.ldb = ld ? ld : ldb0; p.ldc = ld ? ld : c.N;
+      p.M = c.M; p.N = c.N; p.K = c.K; p.tri = c.tri; p.lower_out = c.lower;
+      p.alpha = 1.0; p.beta = 0.0; p.ksplit = 1;
+      const int64_t rowsA = c.al == LAY_N ? c.M : c.K, rowsB = c.bl == LAY_T ? c.N : c.K;
+      if ((double)rowsA * p.lda > 20480.0 * 20480 || (double)rowsB * p.ldb > 20480.0 * 20480 ||
+          (double)c.M * p.ldc > 20480.0 * 20480) { printf("%-28s ld %5ld skipped\n", c.name, (long)ld); continue; }
+      const double fl = c.lower ? (double)c.M * (c.M + 1) * c.K : (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.K;
+      printf("%-28s ld %5ld %7.2f TF/s\n", c.name, (long)(ld ? ld : lda0), run(c.al, c.bl, EPI_STORE, p, 3, fl));
+    }
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 20480;
   double *A, *B, *C, *o0, *o1, *w;
@@ -101,6 +129,7 @@ int main(int argc, char** argv) {
   }
   hipMemset(w, 0, n * 8);
   printf("operands: %s\n", zeros ? "zeros" : "uniform random [-0.5, 0.5)");
+  if (argc > 1 && !strcmp(argv[1], "ld")) return ldstudy(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "sweep")) {
     double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);
     return sweep(A, B, C, ws);
