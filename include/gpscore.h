@@ -68,7 +68,9 @@ enum {
                            the child's leading block is factored while the rest is updated */
   GPS_OPT_RESERVE_CUS = 2, /* CUs (default 0) the off-critical-path streams may not use (CU-masked
                            streams; measured slower on MI355X, kept for experiments) */
-  GPS_OPT_GEMM_MAP = 3    /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
+  GPS_OPT_GEMM_MAP = 3,   /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
+  GPS_OPT_FORK_MIN = 4    /* smallest recursion block (in 128-row blocks, default 1) whose
+                             off-critical-path product is forked to the side stream */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

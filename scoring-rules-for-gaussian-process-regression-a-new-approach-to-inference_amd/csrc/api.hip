@@ -67,6 +67,9 @@ struct gps_ctx {
                                        // (measured neutral on C3: 131.2 vs 130.1 ms; off by default)
   int reserve_cus = 0;                 // GPS_OPT_RESERVE_CUS: CUs kept free of off-path streams
   int gemm_map = 0;                    // GPS_OPT_GEMM_MAP: tile-order override (A/B measurements)
+  int fork_min = 1;                    // GPS_OPT_FORK_MIN: smallest n1 (in 128-blocks) whose T GEMM
+                                       // goes to the side stream (a fork/join costs ~13 us, but
+                                       // forking every level measured best: 128.3 vs 129.1 ms)
   int ncu = 0;
   std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
   size_t sync_used = 0;
@@ -323,10 +326,13 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
                                     (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
   const bool look = ctx->overlap && depth < ctx->lookahead && n2b >= 2;
-  hipStream_t ts = !ctx->overlap ? s : (look ? ctx->look[depth] : ctx->side);
+  // an event fork + join costs ~13 us of dependent-chain latency (tools/launch_latency.hip),
+  // more than the overlap wins for the small T products near the leaves
+  const bool forked = ctx->overlap && (look || n1b >= ctx->fork_min);
+  hipStream_t ts = !forked ? s : (look ? ctx->look[depth] : ctx->side);
   hipEvent_t fork = sync_event(ctx), join = sync_event(ctx), upd = nullptr;
   if (!fork || !join) return fail(ctx, -2, "hipEventCreate failed");
-  if (ctx->overlap) {
+  if (forked) {
     HIPCHK(hipEventRecord(fork, s));
     HIPCHK(hipStreamWaitEvent(ts, fork, 0));
   }
@@ -364,12 +370,12 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
     if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, ts))) return rc;
   }
-  if (ctx->overlap) HIPCHK(hipEventRecord(join, ts));
+  if (forked) HIPCHK(hipEventRecord(join, ts));
   if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W + (int64_t)n1 * n2, n2b, logdiag + n1, info,
                           base + n1, nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr,
                           ldlo, depth + 1, upd)))
     return rc;
-  if (ctx->overlap) HIPCHK(hipStreamWaitEvent(s, join, 0));
+  if (forked) HIPCHK(hipStreamWaitEvent(s, join, 0));
   {  // L⁻¹21 = −L22⁻¹ · T
     GemmParams p = gp0();
     p.A = Li22; p.lda = ldl; p.B = A21; p.ldb = lda; p.C = Li21; p.ldc = ldl;
@@ -563,6 +569,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
     case GPS_OPT_LOOKAHEAD: ctx->lookahead = value < 0 ? 0 : (value > 2 ? 2 : value); return 0;
     case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
+    case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
     case GPS_OPT_RESERVE_CUS:
       ctx->reserve_cus = value < 0 ? 0 : value;
       return make_aux_streams(ctx);
