@@ -194,8 +194,9 @@ def fitc_case(ns, X, y, Xt, yt, Z, log_sf2, log_ell, log_sn2):
     return out
 
 
-def grads_full(ns, X, y, log_sf2, log_ell, log_sn2):
-    """Autograd gradients of the three full-GP objectives (KF:252, 339, 428): for next-1."""
+def grads_full(ns, X, y, log_sf2, log_ell, log_sn2, kern="ARD"):
+    """Autograd gradients of the three full-GP objectives (KF:252, 339, 428): for next-1.
+    kern = "ARD" (b = log ℓ, scalar or per-dimension) or "rbf" (b = log ℓ², SD:8-21)."""
     res = {}
     for obj in ("loo_crps", "nlml", "loo_logs"):
         para_k = T([log_sf2]).requires_grad_(True)
@@ -204,7 +205,7 @@ def grads_full(ns, X, y, log_sf2, log_ell, log_sn2):
         train_x, train_y = T(X), T(y).view(-1, 1)
         n = train_x.shape[0]
         sigma_noise_sq = torch.exp(para_noise)
-        k_ff = ns["ARD"](train_x, train_x, para_k, para_l)
+        k_ff = ns[kern](train_x, train_x, para_k, para_l)
         big_k = k_ff + sigma_noise_sq * torch.eye(n)
         if obj == "nlml":
             hl = torch.linalg.cholesky(big_k, upper=True).diag().log().sum()
@@ -302,10 +303,12 @@ def main():
         X, y, Xt, yt, kblk = simple_data(ns, 100 * j)
         for tag, th in (("init", (1.0, 1.0, 1.0)), ("fit", (0.0, 0.0, math.log(0.09)))):
             o = full_case(ns, X, y, Xt, yt, *th, kern="ARD")
-            save(f"sd_j{j}_{tag}", X=X, y=y, Xt=Xt, yt=yt, theta=np.array(th), kern="ARD", **o)
+            g = grads_full(ns, X, y, *th, kern="ARD")  # SD:199-216: scalar para_l, d = 1
+            save(f"sd_j{j}_{tag}", X=X, y=y, Xt=Xt, yt=yt, theta=np.array(th), kern="ARD", **o, **g)
         o = full_case(ns, X, y, Xt, yt, 0.0, 0.5, math.log(0.09), kern="rbf")
+        g = grads_full(ns, X, y, 0.0, 0.5, math.log(0.09), kern="rbf")
         save(f"sd_j{j}_rbf", X=X, y=y, Xt=Xt, yt=yt, theta=np.array((0.0, 0.5, math.log(0.09))),
-             kern="rbf", k_init_block=kblk, **o)
+             kern="rbf", k_init_block=kblk, **o, **g)
 
     # ---- d = 8 synthetic full-GP cases ------------------------------------------
     d = 8
@@ -317,6 +320,13 @@ def main():
         extra = grads_full(ns, X, y, *th) if n <= 500 else {}
         save(f"full_n{n}_d8", X=X, y=y, Xt=Xt, yt=yt, log_sf2=th[0], log_ell=th[1],
              log_sn2=th[2], **o, **extra)
+
+    # ---- scalar length-scale broadcast over d = 8 (KF:8-12 with para_l of shape [1]) ----
+    X, y, Xt, yt, _ = synth(1064, 64, 64, d)
+    th = (0.2, math.log(1.7), math.log(0.02))
+    o = full_case(ns, X, y, Xt, yt, *th)
+    save("full_n64_d8_iso", X=X, y=y, Xt=Xt, yt=yt, log_sf2=th[0], log_ell=np.array([th[1]]),
+         log_sn2=th[2], **o, **grads_full(ns, X, y, *th))
 
     # ---- FITC cases -------------------------------------------------------------
     for n, nt, mm, zkind in ((64, 64, 5, "rows"), (500, 500, 20, "rows"),

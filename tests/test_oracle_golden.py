@@ -32,6 +32,22 @@ def test_full_oracle_vs_golden(name, flavour):
     _check(out, g, 1e-9)
 
 
+GRAD = [n for n in FULL if "grad_nlml" in load_golden(n)]
+
+
+@pytest.mark.parametrize("name", GRAD)
+@pytest.mark.parametrize("obj", ["nlml", "loo_crps", "loo_logs"])
+def test_oracle_gradients_vs_autograd(name, obj):
+    """Analytic gradients (oracle.fast_full_grad: tr(M ∂A/∂θ)) against the reference's own
+    autograd `.backward()` (KF:252 / KF:339 / KF:428) captured in the goldens:
+    ARD per-dimension ℓ, scalar ℓ broadcast over d, d = 1 (SIMPLE-DATA) and rbf (b = log ℓ²)."""
+    g = load_golden(name)
+    th, kind = theta_of(g)
+    val, grad = O.fast_full_grad(g["X"], g["y"], *th, obj, kind="rbf" if kind == "rbf" else "ARD")
+    assert abs(val - float(g[obj])) <= 1e-10 * max(1.0, abs(float(g[obj])))
+    assert nrel(grad, g["grad_" + obj]) <= 1e-10
+
+
 @pytest.mark.parametrize("name", FITC)
 @pytest.mark.parametrize("flavour", ["ref", "fast", "shard3"])
 def test_fitc_oracle_vs_golden(name, flavour):
