@@ -114,6 +114,14 @@ int gps_full_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t 
  * mu_loo / var_loo (length n) may be NULL (kept on device). */
 int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell,
                  double obj[GPS_N_OBJ], double* mu_loo, double* var_loo);
+/* Forward + analytic gradient of one objective (GPS_OBJ_NLML / _LOO_CRPS / _LOO_LOGS) at
+ * theta: what one GD iteration of the reference computes with autograd `.backward()`
+ * (KF:252 LOO-CRPS, KF:339 NLML, KF:428 LOO-LogS) before its SGD update (KF:254-260).
+ * grad (length 2 + n_ell) = [d/d log sf2, d/d b (n_ell), d/d log sigma2] in the
+ * reference's parameterisation (para_k, para_l, para_noise).  Also leaves the factor
+ * for gps_full_predict, like gps_full_fit. */
+int gps_full_grad(gps_ctx* ctx, int kind, const double* theta, int n_ell, int objective,
+                  double obj[GPS_N_OBJ], double* grad);
 /* Predictive mean/variance at the test points with the last fit's factor
  * (cal_mean_and_cov KF:121-126, diag of the covariance), plus the score bundle
  * against yt (KF:276-292).  mu / var may be NULL; sc may be NULL. */

@@ -88,6 +88,8 @@ struct gps_ctx {
   DBuf X, y, Xt, yt, A, Linv, W, logdiag, beta, alpha, dinv, slab, mu_loo, var_loo, Ksf, s1, s2,
       mu, var, Lout;
   size_t linv_zeroed = 0;
+  int n_ell = 1;
+  DBuf gu, gct, gv, Mx, gslab, gout;  // gradient scratch
   int64_t n = 0, n_pad = 0, nt = 0, nt_pad = 0;
   int d = 0;
   double ytr_mean = 0, ytr_var = 1;
@@ -533,7 +535,8 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
                  &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
-                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_look[0], &ctx->ws_look[1]};
+                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_look[0], &ctx->ws_look[1],
+                 &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
@@ -824,11 +827,11 @@ int gps_full_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t 
   return 0;
 }
 
-int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell, double obj[GPS_N_OBJ],
-                 double* mu_loo, double* var_loo) {
-  if (int rc = bind(ctx)) return rc;
+// Gram + factorisation + β, α, diag(A⁻¹) + LOO sums; objectives land in ctx->small (device)
+int full_fit_core(gps_ctx* ctx, int kind, const double* theta, int n_ell) {
   ARGCHK(ctx->have_data, "gps_full_set_data first");
   if (int rc = set_theta(ctx, ctx->th, kind, theta, n_ell, ctx->d)) return rc;
+  ctx->n_ell = n_ell;
   const int64_t n = ctx->n, np = ctx->n_pad;
   hipStream_t s = ctx->stream;
   HIPCHK(ensure(ctx->A, (size_t)np * np * 8));
@@ -869,6 +872,16 @@ int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell, double 
                            ctx->logdiag.d(), (int)n, ctx->mu_loo.d(), ctx->var_loo.d(),
                            ctx->small.d(), s));
   }
+  return 0;
+}
+
+int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell, double obj[GPS_N_OBJ],
+                 double* mu_loo, double* var_loo) {
+  if (int rc = bind(ctx)) return rc;
+  int rc;
+  if ((rc = full_fit_core(ctx, kind, theta, n_ell))) return rc;
+  const int64_t n = ctx->n;
+  hipStream_t s = ctx->stream;
   HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, GPS_N_OBJ * 8, hipMemcpyDeviceToHost, s));
   if ((rc = check_info(ctx))) return rc;
   if (obj)
@@ -876,6 +889,95 @@ int gps_full_fit(gps_ctx* ctx, int kind, const double* theta, int n_ell, double 
   if (mu_loo) HIPCHK(hipMemcpyAsync(mu_loo, ctx->mu_loo.p, n * 8, hipMemcpyDeviceToHost, s));
   if (var_loo) HIPCHK(hipMemcpyAsync(var_loo, ctx->var_loo.p, n * 8, hipMemcpyDeviceToHost, s));
   if (mu_loo || var_loo) HIPCHK(hipStreamSynchronize(s));
+  ctx->fitted = true;
+  return 0;
+}
+
+// Objective value + analytic gradient (the reference's fwd + `.backward()` of one GD
+// iteration: KF:239-252 LOO-CRPS, KF:329-339 NLML, KF:416-428 LOO-LogS).
+//   grad = [∂/∂log sf², ∂/∂b (n_ell entries), ∂/∂log σ²] = Σ_ij M_ij ∂A_ij/∂θ
+//   NLML: M = ½(A⁻¹ − ααᵀ); LOO: M = −½(vαᵀ + αvᵀ) − A⁻¹ diag(c̃) A⁻¹ (kernels_grad.hip)
+// A⁻¹ = L⁻ᵀL⁻¹ is one triangular SYRK-shaped GEMM (n³/3 flops); the LOO objectives add
+// A⁻¹ diag(c̃) A⁻¹ (n³ flops, lower tiles) and one GEMV.
+int gps_full_grad(gps_ctx* ctx, int kind, const double* theta, int n_ell, int objective,
+                  double obj[GPS_N_OBJ], double* grad) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(grad != nullptr, "grad is NULL");
+  ARGCHK(objective == GPS_OBJ_NLML || objective == GPS_OBJ_LOO_CRPS ||
+             objective == GPS_OBJ_LOO_LOGS,
+         "objective must be GPS_OBJ_NLML, GPS_OBJ_LOO_CRPS or GPS_OBJ_LOO_LOGS");
+  int rc;
+  if ((rc = full_fit_core(ctx, kind, theta, n_ell))) return rc;
+  const int64_t n = ctx->n, np = ctx->n_pad;
+  const int d = ctx->d;
+  hipStream_t s = ctx->stream;
+  {  // A⁻¹ (lower 128-tiles) = L⁻ᵀL⁻¹ into the factorisation's scratch A
+    GemmParams p = gp0();
+    p.A = ctx->Linv.d(); p.lda = np; p.B = ctx->Linv.d(); p.ldb = np;
+    p.C = ctx->A.d(); p.ldc = np;
+    p.M = (int)np; p.N = (int)np; p.K = (int)np; p.tri = TRI_K_GE_I; p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+  }
+  GradParams g;
+  memset(&g, 0, sizeof(g));
+  g.x = ctx->X.d(); g.n = (int)n; g.d = d; g.sf2 = ctx->th.sf2;
+  for (int k = 0; k < d; ++k) g.inv_ell[k] = ctx->th.inv_ell[k];
+  g.Ainv = ctx->A.d(); g.ldm = np; g.alpha = ctx->alpha.d();
+  if (objective == GPS_OBJ_NLML) {
+    g.a0 = 0.5;
+    g.a1 = -0.5;
+  } else {
+    HIPCHK(ensure(ctx->gu, np * 8));
+    HIPCHK(ensure(ctx->gct, np * 8));
+    HIPCHK(ensure(ctx->gv, np * 8));
+    HIPCHK(ensure(ctx->Mx, (size_t)np * np * 8));
+    {
+      Prof pr(ctx, "grad_mirror", 0, 16.0 * (double)np * np / 2);
+      HIPCHK(launch_sym_mirror(ctx->A.d(), np, (int)np, s));
+    }
+      HIPCHK(launch_loo_grad_terms(ctx->y.d(), ctx->alpha.d(), ctx->dinv.d(), (int)n, (int)np,
+                                 objective, ctx->gu.d(), ctx->gct.d(), s));
+    {
+      Prof pr(ctx, "grad_gemv_v", 0, 8.0 * (double)np * np);
+      HIPCHK(launch_gemv_full(ctx->A.d(), np, ctx->gu.d(), ctx->gv.d(), (int)np, (int)np, s));
+    }
+    {  // Mx = A⁻¹ diag(c̃) A⁻¹ (lower tiles): NT with the per-k scale on the A operand
+      GemmParams p = gp0();
+      p.A = ctx->A.d(); p.lda = np; p.B = ctx->A.d(); p.ldb = np;
+      p.C = ctx->Mx.d(); p.ldc = np; p.kscale = ctx->gct.d();
+      p.M = (int)np; p.N = (int)np; p.K = (int)np; p.lower_out = 1;
+      if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
+    }
+    g.a2 = -1.0;
+    g.a3 = -1.0;
+    g.v = ctx->gv.d();
+    g.Mx = ctx->Mx.d();
+  }
+  const int passes = grad_contract_passes(d);
+  HIPCHK(ensure(ctx->gslab, (size_t)grad_contract_slab_doubles((int)n, d) * 8));
+  HIPCHK(ensure(ctx->gout, (size_t)passes * 18 * 8));
+  g.slab = ctx->gslab.d();
+  {
+    Prof pr(ctx, "grad_contract", 0, (objective == GPS_OBJ_NLML ? 8.0 : 16.0) * (double)n * n / 2);
+    HIPCHK(launch_grad_contract(g, ctx->gout.d(), s));
+  }
+  std::vector<double> hout((size_t)passes * 18);
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, GPS_N_OBJ * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hout.data(), ctx->gout.p, hout.size() * 8, hipMemcpyDeviceToHost, s));
+  if ((rc = check_info(ctx))) return rc;  // synchronises the stream
+  if (obj)
+    for (int q = 0; q < GPS_N_OBJ; ++q) obj[q] = ctx->hsmall[q];
+  // ∂A/∂b_k = K ∘ Δ_k² (ARD, b = log ℓ) or ½ K ∘ Δ_k² (RBF, b = log ℓ²); scalar b sums over k
+  const double bscale = kind == GPS_RBF ? 0.5 : 1.0;
+  grad[0] = hout[0];
+  double tot = 0.0;
+  for (int k = 0; k < d; ++k) {
+    const double gk = bscale * hout[(size_t)(k / 16) * 18 + 2 + (k % 16)];
+    if (n_ell == d) grad[1 + k] = gk;
+    tot += gk;
+  }
+  if (n_ell == 1) grad[1] = tot;
+  grad[1 + n_ell] = ctx->th.sn2 * hout[1];
   ctx->fitted = true;
   return 0;
 }

@@ -68,6 +68,50 @@ struct GemmParams {
 struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 
+// ------------------------------------------------------------ device reductions
+// fixed-order wave / block sums (no atomics anywhere: results are bitwise reproducible)
+#ifdef __HIPCC__
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// block-wide sum of NV values per thread; result valid in every thread
+template <int NV>
+__device__ void block_sum(double (&v)[NV], double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = wave_sum(v[q]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) sh[q * 16 + wave] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += sh[q * 16 + w];
+    v[q] = t;
+  }
+  __syncthreads();
+}
+
+#endif
+
+// gradient contraction: Σ_ij M_ij ∂A_ij/∂θ over the real n×n lower triangle with
+// M_ij = a0·Ainv_ij + a1·α_iα_j + a2·½(v_iα_j + α_iv_j) + a3·Mx_ij (kernels_grad.hip)
+struct GradParams {
+  const double* x;          // [n][d] raw features
+  int n, d;
+  double sf2;
+  double inv_ell[GPS_MAX_D];
+  const double* Ainv; const double* Mx; int64_t ldm;
+  const double* alpha; const double* v;
+  double a0, a1, a2, a3;
+  double* slab;             // grad_contract_slab_doubles(n, d)
+};
+
 // ------------------------------------------------------------------ launchers
 hipError_t launch_gram(const GramParams& p, hipStream_t s);
 // C = alpha * op(A) op(B) + beta * C with the epilogue selected by `epi`
@@ -129,5 +173,16 @@ hipError_t launch_dot(const double* a, const double* b, int n, double* out, hipS
 // diagonal (embedding an SPD matrix as diag(A, I))
 hipError_t launch_pad_copy(const double* src, int64_t lds, double* dst, int64_t ldd, int rows,
                            int cols, int rows_pad, int cols_pad, int pad_identity, hipStream_t s);
+
+// --- gradients (kernels_grad.hip)
+// u = −g_μ/d, ct = (g_μα − g_c)/d² of the mean LOO score `obj` (GPS_OBJ_LOO_CRPS / _LOGS)
+hipError_t launch_loo_grad_terms(const double* y, const double* alpha, const double* dinv, int n,
+                                 int n_pad, int obj, double* u, double* ct, hipStream_t s);
+// strictly-upper 32-tiles := transpose of the strictly-lower ones
+hipError_t launch_sym_mirror(double* M, int64_t ld, int n_pad, hipStream_t s);
+int grad_contract_passes(int d);
+int64_t grad_contract_slab_doubles(int n, int d);
+// out[pass*18 + q]: q = 0 Σ w m K, 1 Σ_diag m, 2+k Σ w m K Δ²_(16·pass+k)
+hipError_t launch_grad_contract(const GradParams& p, double* out, hipStream_t s);
 
 }  // namespace gps

@@ -9,32 +9,6 @@
 
 namespace gps {
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-// block-wide sum of NV values per thread; result valid in every thread
-template <int NV>
-__device__ void block_sum(double (&v)[NV], double* sh) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int q = 0; q < NV; ++q) v[q] = wave_sum(v[q]);
-  __syncthreads();
-  if (lane == 0)
-#pragma unroll
-    for (int q = 0; q < NV; ++q) sh[q * 16 + wave] = v[q];
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NV; ++q) {
-    double t = 0.0;
-    for (int w = 0; w < nw; ++w) t += sh[q * 16 + w];
-    v[q] = t;
-  }
-  __syncthreads();
-}
-
 __device__ __forceinline__ double crps_term(double m, double c, double y) {
   const double s = sqrt(c);
   const double z = (y - m) / s;

@@ -48,6 +48,7 @@ SIGNATURES = {
     "gps_full_set_data": (_c_int, [_c_vp, _P, _P, _c_i64, _c_int]),
     "gps_full_set_test": (_c_int, [_c_vp, _P, _P, _c_i64]),
     "gps_full_fit": (_c_int, [_c_vp, _c_int, _P, _c_int, _P, _P, _P]),
+    "gps_full_grad": (_c_int, [_c_vp, _c_int, _P, _c_int, _c_int, _P, _P]),
     "gps_full_predict": (_c_int, [_c_vp, _P, _P, _P]),
     "gps_fitc_set_data": (_c_int, [_c_vp, _P, _P, _c_i64, _c_int, _c_dbl, _c_dbl, _c_i64]),
     "gps_fitc_set_test": (_c_int, [_c_vp, _P, _P, _c_i64, _c_i64]),

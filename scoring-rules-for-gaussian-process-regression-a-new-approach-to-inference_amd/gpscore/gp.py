@@ -132,6 +132,49 @@ class GP:
             self.ctx.call("gps_fitc_fit", ptr(th), n_ell, ptr(obj), ptr(mu), ptr(var))
         return FitResult(self.kind, dict(zip(OBJ_NAMES, obj.tolist())), mu, var)
 
+    # ------------------------------------------------------------- gradients
+    def value_and_grad(self, theta, objective="loo_crps", X=None, y=None, rbf=False):
+        """Objective value and its analytic gradient at theta — the forward body plus the
+        `.backward()` of one GD iteration of the reference (KF:239-252 LOO-CRPS,
+        KF:329-339 NLML, KF:416-428 LOO-LogS).  Returns (value, grad, objectives) with
+        grad = [d/d para_k, d/d para_l (1 or d), d/d para_noise] (full GP only)."""
+        if X is not None:
+            self.set_data(X, y)
+        if self.kind != "full":
+            raise ValueError("analytic gradients are implemented for the full GP")
+        if objective not in OBJ_NAMES[:3]:
+            raise ValueError(f"objective must be one of {OBJ_NAMES[:3]}")
+        th, n_ell = pack_theta(theta, self._X.shape[1])
+        obj = np.zeros(5)
+        grad = np.zeros(2 + n_ell)
+        self.ctx.call("gps_full_grad", GPS_RBF if rbf else GPS_ARD, ptr(th), n_ell,
+                      OBJ_NAMES.index(objective), ptr(obj), ptr(grad))
+        objs = dict(zip(OBJ_NAMES, obj.tolist()))
+        return objs[objective], grad, objs
+
+    def train(self, theta0, objective="loo_crps", lr=1.0, itr=400, X=None, y=None, rbf=False,
+              callback=None):
+        """The reference's GD fit loop (e.g. KF:236-260): `itr` plain SGD steps
+        para -= lr * grad on (para_k, para_l, para_noise), one forward + analytic
+        backward per step on the device.  Returns (theta, series) where series holds the
+        objective value before each step and the parameters after it."""
+        if X is not None:
+            self.set_data(X, y)
+        d = self._X.shape[1]
+        th, n_ell = pack_theta(theta0, d)
+        th = th.copy()
+        values = np.zeros(itr)
+        params = np.zeros((itr, th.size))
+        for i in range(itr):
+            val, g, _ = self.value_and_grad((th[0], th[1:1 + n_ell], th[-1]), objective, rbf=rbf)
+            values[i] = val
+            th -= lr * g
+            params[i] = th
+            if callback is not None:
+                callback(i, val, th)
+        theta = (float(th[0]), th[1:1 + n_ell].copy(), float(th[-1]))
+        return theta, {"objective": values, "theta": params}
+
     # --------------------------------------------------------------- predict
     def predict(self, Xt=None, yt=None, with_scores=False):
         """Predictive mean and variance (the diagonal of cal_mean_and_cov /
