@@ -198,6 +198,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-fitc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-grad", action="store_true")
     ap.add_argument("--lookahead", type=int, default=0,
                     help="recursion depths with a split (lookahead) trailing update; 0 disables")
     ap.add_argument("--reserve-cus", type=int, default=None,
@@ -265,6 +266,22 @@ def main():
         "kernel_accounting": {"ms_per_step": ms_acct, "streams": 1,
                               "note": "second timed pass, overlap off, hipEvents around each launch"},
     }
+
+    # ---------------- gradients (next-1: one GD iteration = fwd + analytic bwd) -------------
+    if not args.no_grad:
+        grad = {}
+        n_pad = -(-c["n"] // 128) * 128
+        for objective, flop in (("nlml", n_pad ** 3 * 1.0), ("loo_crps", n_pad ** 3 * 2.0)):
+            def gstep():
+                return gp.value_and_grad(th, objective)
+            gstep()
+            tg = timed(ctl, ctx, gstep, max(1, args.steps // 2))
+            ms = 1e3 * tg / max(1, args.steps // 2)
+            grad[objective] = {"ms_per_iteration": ms, "flop": flop,
+                               "tflops": flop / (ms * 1e-3) / 1e12}
+        res["grad"] = {"config": args.config, "note": "value_and_grad per GD iteration "
+                       "(fit + A^-1 + [A^-1 diag(c) A^-1] + dA/dtheta contraction); flop = n^3 "
+                       "(NLML) / 2n^3 (LOO) at n_pad", **grad}
 
     # ---------------- FITC (rows sharded, RCCL all-reduce) ----------------
     if not args.no_fitc:

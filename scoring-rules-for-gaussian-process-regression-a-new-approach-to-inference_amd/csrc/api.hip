@@ -229,6 +229,11 @@ const char* gemm_tag(int al, int bl, int epi, const GemmParams& p) {
 // algorithmic flops of one launch (triangular operands counted at their nonzero half)
 double gemm_flops(const GemmParams& p) {
   const double M = p.M, N = p.N, K = p.K;
+  if (p.lower_out && p.tri == TRI_K_GE_I) {  // L⁻ᵀL⁻¹ (LAUUM): k >= i over the lower half
+    double f = 0.0;
+    for (int64_t i = 0; i < p.M; i += GPS_TILE) f += (double)(i + GPS_TILE) * (K - i);
+    return 2.0 * GPS_TILE * f;
+  }
   if (p.lower_out) return M * (M + 1) * K;  // SYRK, lower half
   if (p.tri) return M * N * K;              // triangular operand: half of 2MNK
   return 2.0 * M * N * K;

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--grad", default=None, help="profile value_and_grad(objective) instead")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     ctx = gpscore.Context(0)
@@ -40,6 +41,9 @@ def main():
         def unit():
             gp.fit(theta=th, return_loo=False)
             gp.predict(with_scores=True)
+    if args.grad:
+        def unit():  # noqa: F811
+            gp.value_and_grad(th, args.grad)
     unit()
     ctx.synchronize()
     ctx.set_overlap(False)

@@ -18,6 +18,9 @@ def kern(d, ind="  "):
 
 
 kern(r["kernels_per_step"])
+for obj, g in r.get("grad", {}).items():
+    if isinstance(g, dict):
+        print("GRAD %-9s %.2f ms/iteration  %.1f TF" % (obj, g["ms_per_iteration"], g["tflops"]))
 for leg, f in r.get("fitc", {}).items():
     print("FITC %s: %.2f ms/step  gemm %.1f TF" % (leg, f["ms_per_step"], f["roofline"]["achieved"]))
     kern(f["kernels_per_step"], "    ")
