@@ -221,6 +221,49 @@ def grads_full(ns, X, y, log_sf2, log_ell, log_sn2, kern="ARD"):
     return res
 
 
+def grads_fitc(ns, X, y, Z, log_sf2, log_ell, log_sn2):
+    """Autograd gradients of the three FITC objectives w.r.t. (para_k, para_l, para_noise)
+    and inducing_x — the `.backward()` at K20:236 (LOO-CRPS, body K20:222-234), K20:344
+    (NLML, body K20:329-340) and K20:452 (LOO-LogS, body K20:434-447).  Inducing points are
+    trained parameters in the reference (K20:247)."""
+    res = {}
+    for obj in ("loo_crps", "nlml", "loo_logs"):
+        para_k = T([log_sf2]).requires_grad_(True)
+        para_l = T(np.atleast_1d(log_ell)).view(1, -1).clone().requires_grad_(True)
+        para_noise = T([log_sn2]).requires_grad_(True)
+        inducing_x = T(Z).clone().requires_grad_(True)
+        ns["para_k"], ns["para_l"], ns["dtype"] = para_k, para_l, torch.DoubleTensor
+        train_x, train_y = T(X), T(y).view(-1, 1)
+        n = train_x.shape[0]
+        ARD, Qf, chol_solve = ns["ARD"], ns["Q"], ns["chol_solve"]
+        sigma_noise_sq = torch.exp(para_noise)
+        k_ff = ARD(train_x, train_x, para_k, para_l)
+        Q_ff = Qf(train_x, inducing_x, train_x)
+        G = torch.diag(k_ff - Q_ff + sigma_noise_sq * torch.eye(n)) * torch.eye(n)
+        big_Q = Q_ff + G
+        if obj == "nlml":                                                  # K20:337-340
+            hl = torch.linalg.cholesky(big_Q, upper=True).diag().log().sum()
+            val = (torch.tensor([0.5 * n * np.log(2 * np.pi)]) + hl
+                   + 0.5 * (train_y.transpose(0, 1)).mm(chol_solve(train_y, big_Q)))
+        else:
+            Q_ii_diag = torch.diag(chol_solve(torch.eye(n), big_Q)).view(n, 1)
+            mean_term = train_y - chol_solve(train_y, big_Q) / Q_ii_diag
+            if obj == "loo_crps":                                          # K20:230-234
+                val = ns["crps"](mean_term, 1 / Q_ii_diag, train_y)
+            else:                                                          # K20:441-447
+                small_Q = torch.diag(big_Q).view(n, 1)
+                small_k = torch.diag(k_ff).view(n, 1)
+                cov_term = 1 / Q_ii_diag + sigma_noise_sq - small_Q + small_k
+                val = ns["logs"](mean_term, cov_term, train_y)
+        val.sum().backward()
+        res[f"grad_{obj}"] = np.concatenate([para_k.grad.numpy().ravel(),
+                                             para_l.grad.numpy().ravel(),
+                                             para_noise.grad.numpy().ravel()])
+        res[f"gradZ_{obj}"] = inducing_x.grad.numpy().copy()
+        res[f"value_{obj}"] = float(val.detach().sum())
+    return res
+
+
 def synth(seed, n, nt, d):
     """SURVEY.md §8(d) synthetic generator."""
     rng = np.random.default_rng(seed)
@@ -338,8 +381,19 @@ def main():
             Z = rng2.random((mm, d))
         th = (0.0, log_ell8, math.log(0.01))
         o = fitc_case(ns, X, y, Xt, yt, Z, *th)
+        extra = grads_fitc(ns, X, y, Z, *th) if n <= 500 else {}
         save(f"fitc_n{n}_m{mm}_{zkind}", X=X, y=y, Xt=Xt, yt=yt, Z=Z, log_sf2=th[0],
-             log_ell=th[1], log_sn2=th[2], **o)
+             log_ell=th[1], log_sn2=th[2], **o, **extra)
+
+    # ---- FITC with a scalar length-scale (SF-style para_l of shape [1]) and d = 1 -----
+    for n, mm, dd, th in ((64, 5, 8, (0.3, math.log(1.5), math.log(0.05))),
+                          (120, 5, 1, (0.1, math.log(0.8), math.log(0.09)))):
+        X, y, Xt, yt, rng2 = synth(3000 + n + dd, n, 40, dd)
+        Z = rng2.random((mm, dd))
+        o = fitc_case(ns, X, y, Xt, yt, Z, *th)
+        save(f"fitc_n{n}_m{mm}_d{dd}_iso", X=X, y=y, Xt=Xt, yt=yt, Z=Z, log_sf2=th[0],
+             log_ell=np.array([th[1]]), log_sn2=th[2], **o,
+             **grads_fitc(ns, X, y, Z, *th))
 
     tot = 0
     for name, sz in written:
