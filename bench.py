@@ -327,6 +327,15 @@ def main():
                          "roofline": roofline_mfma(fprof, None, args.steps),
                          "kernel_accounting_ms_per_step": fms_acct,
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
+            if not args.no_grad:  # next-1: one FITC GD iteration (theta and Z), K20:222-247
+                fg = {}
+                for objective in ("nlml", "loo_crps"):
+                    def fgstep():
+                        return fgp.value_and_grad(thf, objective)
+                    fgstep()
+                    k = max(1, args.steps // 2)
+                    fg[objective] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, fgstep, k) / k}
+                fitc[leg]["grad"] = fg
             del Xf, yf, Xtf, ytf
         if world > 1 and not args.rehearse:
             ctx.call("gps_comm_destroy")

@@ -138,6 +138,14 @@ int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m);
  * are then global and mu_loo / var_loo hold this rank's rows. */
 int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
                  double* mu_loo, double* var_loo);
+/* Forward + analytic gradient of one FITC objective w.r.t. theta AND the inducing
+ * inputs: the reference's `.backward()` through its dense FITC bodies at K20:236
+ * (LOO-CRPS), K20:344 (NLML), K20:452 (LOO-LogS) before the SGD step that also moves
+ * inducing_x (K20:238-247).  grad (2 + n_ell) as gps_full_grad; grad_z (m×d, row-major,
+ * may be NULL) = d obj / d Z.  O(n·m²); with a communicator every rank gets the global
+ * gradient. */
+int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
+                  double obj[GPS_N_OBJ], double* grad, double* grad_z);
 int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]);
 
 /* ---- multi-GPU (RCCL over xGMI) ------------------------------------------- */

@@ -98,6 +98,7 @@ struct gps_ctx {
   // ---- FITC state
   DBuf fX, fy, fXt, fyt, Z, Kmm, Am, Lm, Lb, ldm, ldb, Knm, q, lam, ilam, ys, slabB, red, c, tvec,
       r, g, fmu_loo, fvar_loo, Ksm, qm, qb, fmu, fvar, fslab;
+  DBuf fgv, fgm, fgB, fR, fgred, fgslab, fgout;  // FITC gradient scratch
   size_t lm_zeroed = 0, lb_zeroed = 0;
   int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
   int fd = 0;
@@ -1079,9 +1080,34 @@ int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m) {
   return 0;
 }
 
-int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
-                 double* mu_loo, double* var_loo) {
-  if (int rc = bind(ctx)) return rc;
+// split-K SYRK over this shard's rows: dst (lower tiles, strict-upper zeroed) =
+// Kmnᵀ diag(kscale) Knm (+ base).  Every workgroup has the same work, so the grid runs
+// in whole rounds of 512 slots (2 per CU): take the smallest split whose last round is
+// >= 95 % full (528 tiles at m = 4096: ks 3 -> 77 % of the slots busy on average, ks 12
+// -> 95 %), with at least 1024 rows per slice and at most 32 slabs.
+int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* dst) {
+  const int64_t np = ctx->fn_pad, mp = ctx->m_pad, tm = mp / GPS_TILE;
+  const int64_t tiles_lower = tm * (tm + 1) / 2;
+  int ks = 1;
+  for (int k = 1; k <= 32 && (int64_t)k * 1024 <= np; ++k) {
+    const int64_t wg = tiles_lower * k, rounds = (wg + 511) / 512;
+    ks = k;
+    if (wg >= 1024 && (double)wg / (512.0 * rounds) >= 0.95) break;
+  }
+  HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
+  GemmParams p = gp0();
+  p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
+  p.C = ctx->slabB.d(); p.ldc = mp; p.c_kslice_stride = mp * mp;
+  p.M = (int)mp; p.N = (int)mp; p.K = (int)np; p.kscale = kscale;
+  p.lower_out = 1; p.ksplit = ks;
+  if (int rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p)) return rc;
+  Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * mp * mp);
+  HIPCHK(launch_sym_slab_sum(ctx->slabB.d(), mp * mp, ks, (int)mp, base, dst, ctx->stream));
+  return 0;
+}
+
+// forward FITC objectives; leaves Knm, Lm⁻¹, Lb⁻¹, λ, r, g = Knm c, c on the device
+int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ]) {
   ARGCHK(ctx->f_data && ctx->f_z, "gps_fitc_set_data / gps_fitc_set_inducing first");
   if (int rc = set_theta(ctx, ctx->fth, GPS_ARD, theta, n_ell, ctx->fd)) return rc;
   const Theta& th = ctx->fth;
@@ -1114,18 +1140,6 @@ int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_
   HIPCHK(ensure(ctx->tvec, mp * 8));
   const int64_t red_len = mp * mp + mp + 8;
   HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
-  // split-K for the m×m SYRK over n rows.  Every workgroup has the same work, so the
-  // grid runs in whole rounds of 512 slots (2 per CU): take the smallest split whose last
-  // round is >= 95 % full (528 tiles at m = 4096: ks 3 -> 77 % of the slots busy on
-  // average, ks 12 -> 95 %), with at least 1024 rows per slice and at most 32 slabs.
-  const int64_t tiles_lower = tm * (tm + 1) / 2;
-  int ks = 1;
-  for (int k = 1; k <= 32 && (int64_t)k * 1024 <= np; ++k) {
-    const int64_t wg = tiles_lower * k, rounds = (wg + 511) / 512;
-    ks = k;
-    if (wg >= 1024 && (double)wg / (512.0 * rounds) >= 0.95) break;
-  }
-  HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
   const int64_t nchunk = (std::max(np, mp) + 255) / 256;
   const int64_t fslab_len = std::max<int64_t>(tm * np, nchunk * mp * 2);
   HIPCHK(ensure(ctx->fslab, (size_t)fslab_len * 8));
@@ -1161,16 +1175,8 @@ int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_
     HIPCHK(launch_fitc_lambda(ctx->q.d(), ctx->fy.d(), (int)n, (int)np, th.sf2, th.sn2,
                               ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal, s));
   }
-  {  // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs)
-    GemmParams p = gp0();
-    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
-    p.C = ctx->slabB.d(); p.ldc = mp; p.c_kslice_stride = mp * mp;
-    p.M = (int)mp; p.N = (int)mp; p.K = (int)np; p.kscale = ctx->ilam.d();
-    p.lower_out = 1; p.ksplit = ks;
-    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
-    Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * mp * mp);
-    HIPCHK(launch_sym_slab_sum(ctx->slabB.d(), mp * mp, ks, (int)mp, nullptr, Bacc, s));
-  }
+  // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs)
+  if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc))) return rc;
   {  // b_p = Kmnᵀ Λ⁻¹ y
     Prof pr(ctx, "colred_b", 0, 8.0 * np * mp);
     HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ctx->ys.d(), nullptr, bvec,
@@ -1221,10 +1227,194 @@ int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_
     obj[GPS_OBJ_LOGDET] = logdet;
     obj[GPS_OBJ_QUAD] = quad;
   }
+  return 0;
+}
+
+int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
+                 double* mu_loo, double* var_loo) {
+  if (int rc = bind(ctx)) return rc;
+  if (int rc = fitc_fit_core(ctx, theta, n_ell, obj)) return rc;
+  const int64_t n = ctx->fn;
+  hipStream_t s = ctx->stream;
   if (mu_loo) HIPCHK(hipMemcpyAsync(mu_loo, ctx->fmu_loo.p, n * 8, hipMemcpyDeviceToHost, s));
   if (var_loo) HIPCHK(hipMemcpyAsync(var_loo, ctx->fvar_loo.p, n * 8, hipMemcpyDeviceToHost, s));
   if (mu_loo || var_loo) HIPCHK(hipStreamSynchronize(s));
   ctx->f_fitted = true;
+  return 0;
+}
+
+// Objective value + analytic gradient of the FITC objectives w.r.t. θ and the inducing
+// inputs Z — the reference's fwd + `.backward()` at K20:236 (LOO-CRPS), K20:344 (NLML),
+// K20:452 (LOO-LogS); Z is a trained parameter there (K20:247).  Formulas: header of
+// kernels_fitc_grad.hip / oracle.fast_fitc_grad.  Work beyond the forward: two m×m
+// LAUUMs, K·[B⁻¹ | N | Km⁻¹] (6nm² flops; NLML skips N), one or two split-K SYRKs
+// (nm² each), 2-4 m³ GEMMs, and the HBM-bound contraction (reads the n×3m product once).
+// Row-sharded across ranks like the forward: m-vectors, m×m SYRKs and the contraction
+// partials are all-reduced; the m×m (Kmm) contraction is replicated.
+int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
+                  double obj[GPS_N_OBJ], double* grad, double* grad_z) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(grad != nullptr, "grad is NULL");
+  ARGCHK(objective == GPS_OBJ_NLML || objective == GPS_OBJ_LOO_CRPS ||
+             objective == GPS_OBJ_LOO_LOGS,
+         "objective must be GPS_OBJ_NLML, GPS_OBJ_LOO_CRPS or GPS_OBJ_LOO_LOGS");
+  double o[GPS_N_OBJ];
+  int rc;
+  if ((rc = fitc_fit_core(ctx, theta, n_ell, o))) return rc;
+  ctx->f_fitted = true;
+  const Theta& th = ctx->fth;
+  const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
+  const int d = ctx->fd;
+  hipStream_t s = ctx->stream;
+  const bool loo = objective != GPS_OBJ_NLML;
+  const double a = loo ? 0.0 : 0.5;
+  // scratch
+  HIPCHK(ensure(ctx->fgv, (size_t)11 * np * 8));
+  HIPCHK(ensure(ctx->fgm, (size_t)6 * mp * 8));
+  HIPCHK(ensure(ctx->fgB, (size_t)5 * mp * mp * 8));
+  HIPCHK(ensure(ctx->fR, (size_t)np * 3 * mp * 8));
+  HIPCHK(ensure(ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
+  const int passes = fitc_contract_passes(d);
+  const int64_t outlen = (int64_t)passes * 17 + m * d;
+  HIPCHK(ensure(ctx->fgslab, (size_t)std::max(fitc_contract_slab_doubles((int)n, (int)mp, d),
+                                               fitc_contract_slab_doubles((int)m, (int)mp, d)) * 8));
+  HIPCHK(ensure(ctx->fgout, (size_t)(2 * outlen + 8) * 8));
+  double* vbase = ctx->fgv.d();
+  double *alpha = vbase, *dinv = vbase + np, *v = vbase + 2 * np, *ulam = vbase + 3 * np,
+         *h = vbase + 4 * np, *hl2 = vbase + 5 * np, *md = vbase + 6 * np, *s1 = vbase + 7 * np,
+         *s2 = vbase + 8 * np, *s3 = vbase + 9 * np, *zv = vbase + 10 * np;
+  double* mb = ctx->fgm.d();
+  double *tku = mb, *tbt = mb + mp, *what = mb + 2 * mp;
+  double* Bb = ctx->fgB.d();
+  double *Binv = Bb, *Kminv = Bb + mp * mp, *Nm = Bb + 2 * mp * mp, *T1 = Bb + 3 * mp * mp,
+         *KmD = Bb + 4 * mp * mp;
+  double* red = ctx->fgred.d();  // [m×m SYRK | Kᵀv (mp) | Σ M_ii | ...]
+  double* tw = red + mp * mp;
+  double* smd = red + mp * mp + mp;
+  double* out1 = ctx->fgout.d();        // Knm contraction [passes*17 | m*d]
+  double* out2 = out1 + outlen;         // Kmm contraction
+  double* R = ctx->fR.d();
+  const int64_t ldr = 3 * mp;
+  HIPCHK(launch_fitc_grad_terms(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n, (int)np,
+                                objective, (double)ctx->fn_total, alpha, dinv, v, ulam, h, hl2, s));
+  // B⁻¹ = Lb⁻ᵀLb⁻¹, Km⁻¹ = Lm⁻ᵀLm⁻¹ (LAUUM, lower tiles) + mirror
+  const double* Ls[2] = {ctx->Lb.d(), ctx->Lm.d()};
+  double* Is[2] = {Binv, Kminv};
+  for (int w = 0; w < 2; ++w) {
+    GemmParams p = gp0();
+    p.A = Ls[w]; p.lda = mp; p.B = Ls[w]; p.ldb = mp; p.C = Is[w]; p.ldc = mp;
+    p.M = (int)mp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_I; p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+    HIPCHK(launch_sym_mirror(Is[w], mp, (int)mp, s));
+  }
+  if (loo) {  // v = C⁻¹u = u/λ − (K B⁻¹ Kᵀ(u/λ))/λ
+    HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr,
+                         ctx->fslab.d(), s));
+    if (ctx->comm) NCCLCHK(ncclAllReduce(tku, tku, (size_t)mp, ncclFloat64, ncclSum, ctx->comm, s));
+    HIPCHK(launch_gemv_full(Binv, mp, tku, tbt, (int)mp, (int)mp, s));
+    HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, tbt, zv, (int)np, (int)mp, s));
+    HIPCHK(launch_fitc_grad_v(ulam, zv, ctx->lam.d(), (int)n, v, s));
+    // S2 = Kᵀ diag(h/λ²) K
+    if ((rc = fitc_syrk(ctx, hl2, nullptr, red))) return rc;
+  }
+  HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, v, nullptr, tw, nullptr,
+                       ctx->fslab.d(), s));  // Kᵀv
+  if (ctx->comm) {
+    double* r0 = loo ? red : tw;
+    const size_t cnt = loo ? (size_t)(mp * mp + mp) : (size_t)mp;
+    NCCLCHK(ncclAllReduce(r0, r0, cnt, ncclFloat64, ncclSum, ctx->comm, s));
+  }
+  HIPCHK(launch_gemv_full(Kminv, mp, tw, what, (int)mp, (int)mp, s));  // ŵ = Km⁻¹Kᵀv
+  auto gemm_nn = [&](const double* A, int64_t lda, const double* B, double* C, int64_t ldc,
+                     int M) -> int {
+    GemmParams p = gp0();
+    p.A = A; p.lda = lda; p.B = B; p.ldb = mp; p.C = C; p.ldc = ldc;
+    p.M = M; p.N = (int)mp; p.K = (int)mp;
+    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
+  };
+  if (loo) {  // N = B⁻¹ S2 B⁻¹
+    HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
+    if ((rc = gemm_nn(red, mp, Binv, T1, mp, (int)mp))) return rc;
+    if ((rc = gemm_nn(Binv, mp, T1, Nm, mp, (int)mp))) return rc;
+  }
+  // R = K·[B⁻¹ | N | Km⁻¹]
+  if ((rc = gemm_nn(ctx->Knm.d(), mp, Binv, R, ldr, (int)np))) return rc;
+  if (loo && (rc = gemm_nn(ctx->Knm.d(), mp, Nm, R + mp, ldr, (int)np))) return rc;
+  if ((rc = gemm_nn(ctx->Knm.d(), mp, Kminv, R + 2 * mp, ldr, (int)np))) return rc;
+  {
+    Prof pr(ctx, "fitc_grad_mdiag", 0, (loo ? 16.0 : 0.0) * np * mp);
+    HIPCHK(launch_fitc_grad_mdiag(loo ? R + mp : nullptr, ldr, ctx->Knm.d(), mp, (int)mp,
+                                  ctx->lam.d(), ctx->r.d(), dinv, alpha, v, loo ? h : nullptr, a,
+                                  (int)n, (int)np, md, s1, s2, s3, s));
+  }
+  // Kᵀ diag(M_ii) K and Σ M_ii (this shard) → all-reduce
+  if ((rc = fitc_syrk(ctx, md, nullptr, red))) return rc;
+  HIPCHK(launch_dot(md, nullptr, (int)np, smd, s));
+  if (ctx->comm)
+    NCCLCHK(ncclAllReduce(red, red, (size_t)(mp * mp + mp + 1), ncclFloat64, ncclSum, ctx->comm, s));
+  HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
+  if ((rc = gemm_nn(red, mp, Kminv, T1, mp, (int)mp))) return rc;
+  if ((rc = gemm_nn(Kminv, mp, T1, KmD, mp, (int)mp))) return rc;
+  // contraction with ∂Knm/∂θ, ∂Knm/∂Z
+  FitcContractParams cp;
+  memset(&cp, 0, sizeof(cp));
+  cp.d = d;
+  cp.sf2 = th.sf2;
+  for (int k = 0; k < d; ++k) cp.inv_ell[k] = th.inv_ell[k];
+  cp.slab = ctx->fgslab.d();
+  {
+    FitcContractParams p = cp;
+    p.xr = ctx->fX.d(); p.xc = ctx->Z.d(); p.nr = (int)n; p.nc = (int)m; p.nc_pad = (int)mp;
+    p.R[p.nt] = R; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s1;
+    if (loo) { p.R[p.nt] = R + mp; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s2; }
+    p.R[p.nt] = R + 2 * mp; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s3;
+    p.pc[0] = -1.0; p.pv[0] = v; p.qv[0] = ctx->c.d();
+    p.pc[1] = -1.0; p.pv[1] = alpha; p.qv[1] = what;
+    Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * (loo ? 3 : 2) * np * mp);
+    HIPCHK(launch_fitc_grad_contract(p, out1, out1 + passes * 17, s));
+  }
+  if (ctx->comm)
+    NCCLCHK(ncclAllReduce(out1, out1, (size_t)outlen, ncclFloat64, ncclSum, ctx->comm, s));
+  {  // ∂Km/∂θ, ∂Km/∂Z (replicated on every rank; jitter is a constant)
+    FitcContractParams p = cp;
+    p.xr = ctx->Z.d(); p.xc = ctx->Z.d(); p.nr = (int)m; p.nc = (int)m; p.nc_pad = (int)mp;
+    if (a != 0.0) {
+      p.R[p.nt] = Binv; p.ldr[p.nt] = mp; p.coef[p.nt++] = a;
+      p.R[p.nt] = Kminv; p.ldr[p.nt] = mp; p.coef[p.nt++] = -a;
+    }
+    if (loo) { p.R[p.nt] = Nm; p.ldr[p.nt] = mp; p.coef[p.nt++] = 1.0; }
+    p.R[p.nt] = KmD; p.ldr[p.nt] = mp; p.coef[p.nt++] = 1.0;
+    p.pc[0] = 0.5; p.pv[0] = what; p.qv[0] = ctx->c.d();
+    p.pc[1] = 0.5; p.pv[1] = ctx->c.d(); p.qv[1] = what;
+    Prof pr(ctx, "fitc_grad_contract_mm", 0, 8.0 * p.nt * mp * mp);
+    HIPCHK(launch_fitc_grad_contract(p, out2, out2 + passes * 17, s));
+  }
+  std::vector<double> hout((size_t)2 * outlen + 1);
+  HIPCHK(hipMemcpyAsync(hout.data(), out1, (size_t)2 * outlen * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hout.data() + 2 * outlen, smd, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const double* h1 = hout.data();
+  const double* h2 = h1 + outlen;
+  const double sum_md = hout[2 * outlen];
+  if (obj)
+    for (int q = 0; q < GPS_N_OBJ; ++q) obj[q] = o[q];
+  grad[0] = h1[0] + h2[0] + th.sf2 * sum_md;
+  double tot = 0.0;
+  for (int k = 0; k < d; ++k) {
+    const size_t at = (size_t)(k / 16) * 17 + 1 + (k % 16);
+    const double gk = h1[at] + h2[at];
+    if (n_ell == d) grad[1 + k] = gk;
+    tot += gk;
+  }
+  if (n_ell == 1) grad[1] = tot;
+  grad[1 + n_ell] = th.sn2 * sum_md;
+  if (grad_z) {
+    const double* z1 = h1 + passes * 17;
+    const double* z2 = h2 + passes * 17;
+    for (int64_t j = 0; j < m; ++j)
+      for (int k = 0; k < d; ++k)
+        grad_z[j * d + k] = (z1[j * d + k] + 2.0 * z2[j * d + k]) * th.inv_ell[k];
+  }
   return 0;
 }
 

@@ -112,6 +112,21 @@ struct GradParams {
   double* slab;             // grad_contract_slab_doubles(n, d)
 };
 
+// FITC gradient contraction (kernels_fitc_grad.hip): rows xr (nr), columns xc (nc),
+// G_ij = Σ_t coef_t·(rs_t ? rs_t[i] : 1)·R_t[i][j] + Σ_q pc_q·pv_q[i]·qv_q[j]
+struct FitcContractParams {
+  const double* xr; const double* xc;   // [nr][d], [nc][d] raw features
+  int nr, nc, nc_pad, d;
+  double sf2;
+  double inv_ell[GPS_MAX_D];
+  int nt;                               // matrix terms (<= 4)
+  const double* R[4]; int64_t ldr[4]; double coef[4]; const double* rs[4];
+  double pc[2]; const double* pv[2]; const double* qv[2];  // rank-1 terms (pc = 0: off)
+  double* slab;                         // fitc_contract_slab_doubles(nr, nc_pad, d)
+  double* zslab;                        // set by the launcher
+  int rchunk;                           // set by the launcher
+};
+
 // ------------------------------------------------------------------ launchers
 hipError_t launch_gram(const GramParams& p, hipStream_t s);
 // C = alpha * op(A) op(B) + beta * C with the epilogue selected by `epi`
@@ -184,5 +199,23 @@ int grad_contract_passes(int d);
 int64_t grad_contract_slab_doubles(int n, int d);
 // out[pass*18 + q]: q = 0 Σ w m K, 1 Σ_diag m, 2+k Σ w m K Δ²_(16·pass+k)
 hipError_t launch_grad_contract(const GradParams& p, double* out, hipStream_t s);
+
+// --- FITC gradients (kernels_fitc_grad.hip)
+hipError_t launch_fitc_grad_terms(const double* y, const double* lam, const double* r,
+                                  const double* g, int n, int n_pad, int obj, double n_total,
+                                  double* alpha, double* dinv, double* v, double* ulam, double* h,
+                                  double* hl2, hipStream_t s);
+hipError_t launch_fitc_grad_v(const double* ulam, const double* z, const double* lam, int n,
+                              double* v, hipStream_t s);
+hipError_t launch_fitc_grad_mdiag(const double* KN, int64_t ldkn, const double* K, int64_t ldk,
+                                  int m_pad, const double* lam, const double* r, const double* dinv,
+                                  const double* alpha, const double* v, const double* h, double a,
+                                  int n, int n_pad, double* mdiag, double* s1, double* s2,
+                                  double* s3, hipStream_t s);
+int fitc_contract_passes(int d);
+int64_t fitc_contract_slab_doubles(int nr, int nc_pad, int d);
+// out[pass*17 + q]: q = 0 Σ GK, 1+k Σ GK Δ²_(16·pass+k);  zout[j*d + k] = Σ_i GK Δ_k (real j)
+hipError_t launch_fitc_grad_contract(FitcContractParams p, double* out, double* zout,
+                                     hipStream_t s);
 
 }  // namespace gps

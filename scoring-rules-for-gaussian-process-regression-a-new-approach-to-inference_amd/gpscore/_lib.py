@@ -54,6 +54,7 @@ SIGNATURES = {
     "gps_fitc_set_test": (_c_int, [_c_vp, _P, _P, _c_i64, _c_i64]),
     "gps_fitc_set_inducing": (_c_int, [_c_vp, _P, _c_i64]),
     "gps_fitc_fit": (_c_int, [_c_vp, _P, _c_int, _P, _P, _P]),
+    "gps_fitc_grad": (_c_int, [_c_vp, _P, _c_int, _c_int, _P, _P, _P]),
     "gps_fitc_predict": (_c_int, [_c_vp, _P, _P, _P]),
     "gps_comm_unique_id": (_c_int, [_c_cp]),
     "gps_comm_init": (_c_int, [_c_vp, _c_int, _c_int, _c_cp]),

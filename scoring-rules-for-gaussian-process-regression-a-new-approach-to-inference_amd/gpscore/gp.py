@@ -133,47 +133,75 @@ class GP:
         return FitResult(self.kind, dict(zip(OBJ_NAMES, obj.tolist())), mu, var)
 
     # ------------------------------------------------------------- gradients
-    def value_and_grad(self, theta, objective="loo_crps", X=None, y=None, rbf=False):
+    def value_and_grad(self, theta, objective="loo_crps", X=None, y=None, rbf=False, Z=None):
         """Objective value and its analytic gradient at theta — the forward body plus the
-        `.backward()` of one GD iteration of the reference (KF:239-252 LOO-CRPS,
-        KF:329-339 NLML, KF:416-428 LOO-LogS).  Returns (value, grad, objectives) with
-        grad = [d/d para_k, d/d para_l (1 or d), d/d para_noise] (full GP only)."""
+        `.backward()` of one GD iteration of the reference (full GP: KF:239-252 LOO-CRPS,
+        KF:329-339 NLML, KF:416-428 LOO-LogS; FITC: K20:222-236, 329-344, 434-452).
+        Returns (value, grad, objectives) with grad = [d/d para_k, d/d para_l (1 or d),
+        d/d para_noise]; for FITC ``objectives["grad_Z"]`` holds d/d inducing_x (m×d),
+        the inducing inputs being trained parameters there (K20:247)."""
         if X is not None:
-            self.set_data(X, y)
-        if self.kind != "full":
-            raise ValueError("analytic gradients are implemented for the full GP")
+            self.set_data(X, y, kind="fitc" if Z is not None else "full", Z=Z)
+        elif Z is not None:
+            self.set_inducing(Z)
         if objective not in OBJ_NAMES[:3]:
             raise ValueError(f"objective must be one of {OBJ_NAMES[:3]}")
         th, n_ell = pack_theta(theta, self._X.shape[1])
         obj = np.zeros(5)
         grad = np.zeros(2 + n_ell)
+        if self.kind == "fitc":
+            if rbf:
+                raise ValueError("FITC uses the ARD kernel (K20:32-39)")
+            if self._Z is None:
+                raise ValueError("FITC needs inducing points Z")
+            gz = np.zeros_like(self._Z)
+            self.ctx.call("gps_fitc_grad", ptr(th), n_ell, OBJ_NAMES.index(objective), ptr(obj),
+                          ptr(grad), ptr(gz))
+            objs = dict(zip(OBJ_NAMES, obj.tolist()))
+            objs["grad_Z"] = gz
+            return objs[objective], grad, objs
         self.ctx.call("gps_full_grad", GPS_RBF if rbf else GPS_ARD, ptr(th), n_ell,
                       OBJ_NAMES.index(objective), ptr(obj), ptr(grad))
         objs = dict(zip(OBJ_NAMES, obj.tolist()))
         return objs[objective], grad, objs
 
     def train(self, theta0, objective="loo_crps", lr=1.0, itr=400, X=None, y=None, rbf=False,
-              callback=None):
-        """The reference's GD fit loop (e.g. KF:236-260): `itr` plain SGD steps
-        para -= lr * grad on (para_k, para_l, para_noise), one forward + analytic
-        backward per step on the device.  Returns (theta, series) where series holds the
-        objective value before each step and the parameters after it."""
+              callback=None, Z0=None, lr_z=None):
+        """The reference's GD fit loop: `itr` plain SGD steps para -= lr * grad on
+        (para_k, para_l, para_noise) — full GP e.g. KF:236-260 — one forward + analytic
+        backward per step on the device.  FITC (K20:219-251, 324-354, 428-458) also moves
+        the inducing inputs: inducing_x -= lr_z * grad_Z (lr_z defaults to lr; the
+        reference uses 1 / 0.001 / 0.2 for LOO-CRPS / NLML / LOO-LogS, K20:221, 327, 431).
+        Returns (theta, series); series holds the objective value before each step, the
+        parameters after it and, for FITC, the final inducing inputs under "Z"."""
         if X is not None:
-            self.set_data(X, y)
+            self.set_data(X, y, kind="fitc" if Z0 is not None else "full", Z=Z0)
+        elif Z0 is not None:
+            self.set_inducing(Z0)
         d = self._X.shape[1]
         th, n_ell = pack_theta(theta0, d)
         th = th.copy()
+        fitc = self.kind == "fitc"
+        lr_z = lr if lr_z is None else lr_z
+        Z = self._Z.copy() if fitc else None
         values = np.zeros(itr)
         params = np.zeros((itr, th.size))
         for i in range(itr):
-            val, g, _ = self.value_and_grad((th[0], th[1:1 + n_ell], th[-1]), objective, rbf=rbf)
+            val, g, objs = self.value_and_grad((th[0], th[1:1 + n_ell], th[-1]), objective,
+                                               rbf=rbf)
             values[i] = val
             th -= lr * g
             params[i] = th
+            if fitc:
+                Z -= lr_z * objs["grad_Z"]
+                self.set_inducing(Z)
             if callback is not None:
                 callback(i, val, th)
         theta = (float(th[0]), th[1:1 + n_ell].copy(), float(th[-1]))
-        return theta, {"objective": values, "theta": params}
+        series = {"objective": values, "theta": params}
+        if fitc:
+            series["Z"] = Z
+        return theta, series
 
     # --------------------------------------------------------------- predict
     def predict(self, Xt=None, yt=None, with_scores=False):
