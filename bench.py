@@ -203,6 +203,8 @@ def main():
                     help="recursion depths with a split (lookahead) trailing update; 0 disables")
     ap.add_argument("--reserve-cus", type=int, default=None,
                     help="CUs kept free of the off-critical-path streams (library default 16)")
+    ap.add_argument("--fused-splitk", action="store_true",
+                    help="in-launch split-K combine instead of the separate reduce kernel")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
@@ -214,6 +216,8 @@ def main():
     import gpscore
     ctx = gpscore.Context(0 if args.rehearse else local)
     ctx.set_lookahead(args.lookahead)
+    if args.fused_splitk:
+        ctx.set_fused_splitk(True)
     if args.reserve_cus is not None:
         ctx.set_reserved_cus(args.reserve_cus)
     gp = gpscore.GP(ctx=ctx)

@@ -69,8 +69,12 @@ enum {
   GPS_OPT_RESERVE_CUS = 2, /* CUs (default 0) the off-critical-path streams may not use (CU-masked
                            streams; measured slower on MI355X, kept for experiments) */
   GPS_OPT_GEMM_MAP = 3,   /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
-  GPS_OPT_FORK_MIN = 4    /* smallest recursion block (in 128-row blocks, default 1) whose
+  GPS_OPT_FORK_MIN = 4,   /* smallest recursion block (in 128-row blocks, default 1) whose
                              off-critical-path product is forked to the side stream */
+  GPS_OPT_FUSED_SPLITK = 5 /* 1: split-K GEMM slabs are combined inside the launch by the
+                             last-arriving slice (agent-scope release/acquire ticket); 0 (default,
+                             measured faster on C3): a separate ordered reduce kernel.  Same
+                             numerics either way. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -67,6 +67,11 @@ struct gps_ctx {
                                        // (measured neutral on C3: 131.2 vs 130.1 ms; off by default)
   int reserve_cus = 0;                 // GPS_OPT_RESERVE_CUS: CUs kept free of off-path streams
   int gemm_map = 0;                    // GPS_OPT_GEMM_MAP: tile-order override (A/B measurements)
+  int fused_splitk = 0;                // GPS_OPT_FUSED_SPLITK: split-K slabs combined in-launch by
+                                       // the last-arriving slice.  Measured slower on C3 (142.1 vs
+                                       // 135.9 ms same box): the last slice reads ks x 32 KB of
+                                       // slabs serially at the cross-XCD rate, ~4 us per tile,
+                                       // more than the reduce launch it removes.  Off by default.
   int fork_min = 1;                    // GPS_OPT_FORK_MIN: smallest n1 (in 128-blocks) whose T GEMM
                                        // goes to the side stream (a fork/join costs ~13 us, but
                                        // forking every level measured best: 128.3 vs 129.1 ms)
@@ -249,9 +254,13 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
                : st == ctx->look[0] ? ctx->ws_look[0]
                : st == ctx->look[1] ? ctx->ws_look[1]
                                     : ctx->ws_main;
-    HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8));
+    if (ws.cap < (size_t)kSplitWsDoubles * 8 + GPS_SPLITK_TICKETS * 4) {
+      HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8 + GPS_SPLITK_TICKETS * 4));
+      HIPCHK(hipMemsetAsync(ws.d() + kSplitWsDoubles, 0, GPS_SPLITK_TICKETS * 4, st));
+    }
     q.ws = ws.d();
     q.ws_cap = kSplitWsDoubles;
+    q.cnt = ctx->fused_splitk ? reinterpret_cast<unsigned*>(ws.d() + kSplitWsDoubles) : nullptr;
   }
   std::string tag = gemm_tag(al, bl, epi, p);
   if (ctx->prof > 1) {  // per-shape accounting (gps_prof_enable(ctx, 2))
@@ -579,6 +588,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_LOOKAHEAD: ctx->lookahead = value < 0 ? 0 : (value > 2 ? 2 : value); return 0;
     case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
+    case GPS_OPT_FUSED_SPLITK: ctx->fused_splitk = value != 0; return 0;
     case GPS_OPT_RESERVE_CUS:
       ctx->reserve_cus = value < 0 ? 0 : value;
       return make_aux_streams(ctx);

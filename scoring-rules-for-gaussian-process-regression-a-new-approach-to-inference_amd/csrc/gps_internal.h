@@ -11,6 +11,7 @@
 
 #define GPS_TILE 128
 #define GPS_MAX_D 64
+#define GPS_SPLITK_TICKETS 16384
 
 namespace gps {
 
@@ -62,6 +63,10 @@ struct GemmParams {
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
+  unsigned* cnt;             // split-K tile tickets (>= GPS_SPLITK_TICKETS, zeroed): the slice
+                             // that draws ksplit-1 sums the slabs in slice order (in-launch)
+  // in-launch combine target (set by launch_gemm): C = alpha_f * Σ slabs + beta_f * C
+  double* Cf; int64_t ldcf; double alpha_f, beta_f;
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark

@@ -292,3 +292,30 @@ def test_profiler_collect(gpu_ctx):
     gpu_ctx.prof(False)
     assert "potrf_diag128" in rep and "gram_kff" in rep and "gemm_trmm_colred" in rep
     assert all(v["ms"] >= 0 for v in rep.values())
+
+
+def test_fused_splitk_bitwise(gpu_ctx):
+    """The in-launch split-K combine (agent-scope release/acquire ticket, last slice sums
+    the slabs in slice order) gives bitwise the same fit, predict and gradient as the
+    separate ordered reduce kernel: n = 3000 exercises split-K at every small recursion
+    level, repeated to shake out arrival orders."""
+    import gpscore
+    rng = np.random.default_rng(5)
+    n, nt, d = 3000, 700, 8
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
+    y = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n)
+    th = (0.0, np.log(np.linspace(1.0, 2.0, d)), np.log(0.01))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    gp.set_data(X, y)
+    gp.set_test(Xt)
+    outs = []
+    for fused in (False, True, True, True):
+        gpu_ctx.set_fused_splitk(fused)
+        r = gp.fit(theta=th)
+        mu, var = gp.predict()
+        _, g, _ = gp.value_and_grad(th, "loo_crps")
+        outs.append((r.mu_loo, r.var_loo, mu, var, g))
+    gpu_ctx.set_fused_splitk(False)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
