@@ -71,10 +71,13 @@ enum {
   GPS_OPT_GEMM_MAP = 3,   /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
   GPS_OPT_FORK_MIN = 4,   /* smallest recursion block (in 128-row blocks, default 1) whose
                              off-critical-path product is forked to the side stream */
-  GPS_OPT_FUSED_SPLITK = 5 /* 1: split-K GEMM slabs are combined inside the launch by the
+  GPS_OPT_FUSED_SPLITK = 5, /* 1: split-K GEMM slabs are combined inside the launch by the
                              last-arriving slice (agent-scope release/acquire ticket); 0 (default,
                              measured faster on C3): a separate ordered reduce kernel.  Same
                              numerics either way. */
+  GPS_OPT_MAIN_CU_EXCLUDE = 6 /* recreate the context's own main stream CU-masked so that the
+                             top `value` CU ids (r/8 per XCD) stay free for other streams/
+                             contexts (0 = unmasked, the default).  For co-scheduling studies. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

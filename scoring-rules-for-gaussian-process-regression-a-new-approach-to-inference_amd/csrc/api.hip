@@ -589,6 +589,20 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
     case GPS_OPT_FUSED_SPLITK: ctx->fused_splitk = value != 0; return 0;
+    case GPS_OPT_MAIN_CU_EXCLUDE: {  // recreate the (owned) main stream CU-masked
+      ARGCHK(ctx->own_stream, "the main stream is caller-owned");
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      HIPCHK(hipStreamDestroy(ctx->stream));
+      const int ncu = ctx->ncu, r = std::max(0, std::min(value, ncu / 2));
+      if (r == 0) {
+        HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+      } else {
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu - r; ++i) mask[i / 32] |= 1u << (i % 32);
+        HIPCHK(hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mask.size(), mask.data()));
+      }
+      return 0;
+    }
     case GPS_OPT_RESERVE_CUS:
       ctx->reserve_cus = value < 0 ? 0 : value;
       return make_aux_streams(ctx);

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_LOOKAHEAD, GPS_OPT_RESERVE_CUS, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN = 0, 1, 2, 3, 4
-GPS_OPT_FUSED_SPLITK = 5
+GPS_OPT_FUSED_SPLITK, GPS_OPT_MAIN_CU_EXCLUDE = 5, 6
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
