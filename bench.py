@@ -205,6 +205,8 @@ def main():
                     help="CUs kept free of the off-critical-path streams (library default 16)")
     ap.add_argument("--fused-splitk", action="store_true",
                     help="in-launch split-K combine instead of the separate reduce kernel")
+    ap.add_argument("--no-tiny-gemm", action="store_true",
+                    help="64-tile split-K path for the small GEMMs instead of the 16x16-per-wave kernel")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
@@ -218,6 +220,8 @@ def main():
     ctx.set_lookahead(args.lookahead)
     if args.fused_splitk:
         ctx.set_fused_splitk(True)
+    if args.no_tiny_gemm:
+        ctx.set_tiny_gemm(False)
     if args.reserve_cus is not None:
         ctx.set_reserved_cus(args.reserve_cus)
     gp = gpscore.GP(ctx=ctx)

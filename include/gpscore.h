@@ -75,7 +75,10 @@ enum {
                              last-arriving slice (agent-scope release/acquire ticket); 0 (default,
                              measured faster on C3): a separate ordered reduce kernel.  Same
                              numerics either way. */
-  GPS_OPT_MAIN_CU_EXCLUDE = 6 /* recreate the context's own main stream CU-masked so that the
+  GPS_OPT_TINY_GEMM = 7,   /* 1 (default): GEMMs with M·N <= 256² and K <= 1024 (the bottom of
+                             the recursion) use the one-wave-per-16×16-tile kernel; 0: 64-tile
+                             split-K + reduce.  Process-wide. */
+  GPS_OPT_MAIN_CU_EXCLUDE = 6, /* recreate the context's own main stream CU-masked so that the
                              top `value` CU ids (r/8 per XCD) stay free for other streams/
                              contexts (0 = unmasked, the default).  For co-scheduling studies. */
 };

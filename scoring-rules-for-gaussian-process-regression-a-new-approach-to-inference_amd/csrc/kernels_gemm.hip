@@ -365,6 +365,97 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   }
 }
 
+// Latency-optimised GEMM for the bottom of the recursion (M·N <= 256², K <= 1024): one
+// wave per 16×16 output tile, operands streamed straight from L2 into MFMA registers (no
+// LDS, no K split, no reduction launch).  For 16-deep K chunks lane l (r = l & 15,
+// g = l >> 4) feeds MFMA step kk with k = 4g + kk of A row r and B column r — a fixed
+// permutation of k inside the chunk shared by both operands, so row-major A / Bᵀ
+// fragments are one contiguous 32-byte load per lane.  Chain per wave: K/4 MFMAs (32 at
+// K = 128, ~0.9 µs) against ~11 µs for the 64-tile split-K kernel + ordered reduce.
+// lower_out enumerates the 16-tiles of the lower 64-tiles (diagonal 64-tiles whole, as
+// the 64/128-tile kernels write them).
+template <int ALAY, int BLAY>
+__global__ __launch_bounds__(256) void gemm_f64_tiny_kernel(GemmParams p) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tm = p.M / 16, tn = p.N / 16;
+  int ti, tj;
+  if (p.lower_out) {  // 16-tiles (ti, tj) with tj/4 <= ti/4, row-major over ti
+    // rows of 16-tiles ti contain 4·(ti/4 + 1) tiles; prefix S(ti) = 4·Σ_{q<ti}(q/4 + 1)
+    int lo = 0, hi = tm;
+    auto pre = [](int r) { const int a = r / 4, b = r % 4; return 4 * (4 * a * (a + 1) / 2 + b * (a + 1)); };
+    if (t >= pre(tm)) return;
+    while (hi - lo > 1) { const int mid = (lo + hi) / 2; if (pre(mid) <= t) lo = mid; else hi = mid; }
+    ti = lo;
+    tj = t - pre(ti);
+  } else {
+    if (t >= tm * tn) return;
+    ti = t / tn;
+    tj = t - ti * tn;
+  }
+  const int row0 = ti * 16, col0 = tj * 16;
+  int kb = 0, ke = p.K;
+  switch (p.tri) {
+    case TRI_K_LE_I: ke = min(ke, row0 + 16); break;
+    case TRI_K_LE_J: ke = min(ke, col0 + 16); break;
+    case TRI_K_GE_J: kb = col0; break;
+    case TRI_K_GE_I: kb = row0; break;
+    default: break;
+  }
+  const int r = lane & 15, g = lane >> 4;
+  auto load = [&](int k0, double (&a)[4], double (&b)[4]) {
+    const int k = k0 + 4 * g;
+    if constexpr (ALAY == LAY_N) {
+      const dv2* s = reinterpret_cast<const dv2*>(p.A + (int64_t)(row0 + r) * p.lda + k);
+      const dv2 u = s[0], v = s[1];
+      a[0] = u.x; a[1] = u.y; a[2] = v.x; a[3] = v.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = p.A[(int64_t)(k + q) * p.lda + row0 + r];
+    }
+    if constexpr (BLAY == LAY_T) {
+      const dv2* s = reinterpret_cast<const dv2*>(p.B + (int64_t)(col0 + r) * p.ldb + k);
+      const dv2 u = s[0], v = s[1];
+      b[0] = u.x; b[1] = u.y; b[2] = v.x; b[3] = v.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[q] = p.B[(int64_t)(k + q) * p.ldb + col0 + r];
+    }
+  };
+  d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+  double a0[4], b0[4], a1[4], b1[4];
+  int k0 = kb;
+  if (k0 < ke) load(k0, a0, b0);
+  while (k0 < ke) {
+    const bool more = k0 + 16 < ke;
+    if (more) load(k0 + 16, a1, b1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[kk], b0[kk], acc, 0, 0, 0);
+    k0 += 16;
+    if (!more) break;
+    const bool more2 = k0 + 16 < ke;
+    if (more2) load(k0 + 16, a0, b0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[kk], b1[kk], acc, 0, 0, 0);
+    k0 += 16;
+    if (!more2) break;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double* c = p.C + (int64_t)(row0 + g + 4 * q) * p.ldc + col0 + r;
+    double v = p.alpha * acc[q];
+    if (p.beta != 0.0) v = fma(p.beta, *c, v);
+    *c = v;
+  }
+}
+
+static int64_t tiny_tiles(const GemmParams& p) {
+  const int64_t tm = p.M / 16, tn = p.N / 16;
+  if (!p.lower_out) return tm * tn;
+  const int64_t a = tm / 4;  // lower 64-tiles, 16 sub-tiles each (M multiple of 128)
+  return 16 * a * (a + 1) / 2;
+}
+
 // C = beta*C + alpha * sum_s slab_s, slabs summed in slice order (deterministic);
 // lower_tile > 0: only tiles with tj <= ti at that tile edge (the rest of a SYRK slab is unwritten)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __restrict__ ws, int ks,
@@ -384,6 +475,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
   *c = v;
 }
 
+int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
+
 static int64_t tiles_for(const GemmParams& p, int tile) {
   const int64_t tm = p.M / tile, tn = p.N / tile;
   return p.lower_out ? tm * (tm + 1) / 2 : tm * tn;
@@ -400,6 +493,7 @@ static int64_t tiles_for(const GemmParams& p, int tile) {
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap) {
   if (p.tile) return {p.tile, p.ksplit > 1 ? p.ksplit : 1};
   if (epi != EPI_STORE || p.ksplit > 1) return {128, p.ksplit > 1 ? p.ksplit : 1};
+  if (g_tiny_gemm && !p.kscale && (int64_t)p.M * p.N <= 256 * 256 && p.K <= 1024) return {16, 1};
   if (tiles_for(p, 128) >= 1024) return {128, 1};
   const int64_t t64 = tiles_for(p, 64);
   const int64_t target = p.lower_out ? 2048 : 1024;
@@ -419,6 +513,15 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   if (p.ksplit < 1) p.ksplit = 1;
   const GemmPlan plan = gemm_plan(epi, p, p.ws ? p.ws_cap : 0);
   const int tile = plan.tile;
+  if (tile == 16) {
+    const int64_t tt = tiny_tiles(p);
+    const dim3 grid((unsigned)((tt + 3) / 4)), block(256);
+    if (alay == LAY_N && blay == LAY_T) hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_N, LAY_T>), grid, block, 0, s, p);
+    else if (alay == LAY_N && blay == LAY_N) hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_N, LAY_N>), grid, block, 0, s, p);
+    else if (alay == LAY_T && blay == LAY_N) hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_T, LAY_N>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_T, LAY_T>), grid, block, 0, s, p);
+    return hipGetLastError();
+  }
   if (tile != 64 && tile != 128) return hipErrorInvalidValue;
   if (tile == 64 && epi != EPI_STORE) return hipErrorInvalidValue;
   p.ksplit = plan.ksplit;
