@@ -40,7 +40,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 # four scripts; rbf exists only in SD/SF)
 SOURCES = {
     "kin40k-FULL-compare.py": ["ARD", "chol_solve", "Q", "crps", "logs",
-                               "trivial_loss", "cal_mean_and_cov", "SMSE"],
+                               "trivial_loss", "cal_mean_and_cov", "SMSE", "dss"],
     "KIN40K-COMPARE-ALL-FITC-20.py": ["spgp_cal_mean_and_cov"],
     "SIMPLE-DATA FULL-comapre.py": ["rbf"],
 }
@@ -81,6 +81,15 @@ def load_reference_defs():
             raise SystemExit(f"defs {missing} not found in {fname}")
         mod = ast.Module(body=list(found.values()), type_ignores=[])
         exec(compile(mod, f"<reference:{fname}>", "exec"), ns)
+    # K20 has its own dss (cov_term.inverse() instead of chol_solve, K20:106-111): load it
+    # under another name for the FITC block-LOO bodies
+    for fname, name, alias in (("KIN40K-COMPARE-ALL-FITC-20.py", "dss", "dss_k20"),):
+        with open(os.path.join(REF, fname), "r", encoding="utf-8", errors="replace") as fh:
+            tree = ast.parse(fh.read().replace("\r\n", "\n"))
+        node = next(n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name)
+        sub = {"torch": ns["torch"], "math": math, "np": np, "chol_solve": ns["chol_solve"]}
+        exec(compile(ast.Module(body=[node], type_ignores=[]), f"<reference:{fname}>", "exec"), sub)
+        ns[alias] = sub[name]
     return ns
 
 
@@ -264,6 +273,63 @@ def grads_fitc(ns, X, y, Z, log_sf2, log_ell, log_sn2):
     return res
 
 
+def block_loo_case(ns, X, y, log_sf2, log_ell, log_sn2, Z=None, with_grad=True):
+    """4-fold block-LOO objectives composed exactly as the scripts write them: full GP DSS
+    (KF:494-543, dss KF:103-108), FITC DSS (K20:536-587, dss K20:106-111) and FITC KC
+    (K20:669-720); "kc" on the full GP applies the K20:682-714 KC body to big_k.  Returns
+    values and autograd gradients (θ; and inducing_x for FITC)."""
+    out = {}
+    for obj in ("dss", "kc"):
+        para_k = T([log_sf2]).requires_grad_(True)
+        para_l = T(np.atleast_1d(log_ell)).view(1, -1).clone().requires_grad_(True)
+        para_noise = T([log_sn2]).requires_grad_(True)
+        ns["para_k"], ns["para_l"], ns["dtype"] = para_k, para_l, torch.DoubleTensor
+        train_x, train_y = T(X), T(y).view(-1, 1)
+        num_train = train_x.shape[0]
+        chol_solve, crps = ns["chol_solve"], ns["crps"]
+        sigma_noise_sq = torch.exp(para_noise)
+        k_ff = ns["ARD"](train_x, train_x, para_k, para_l)
+        fold_k = 4
+        index1 = int(num_train / fold_k)
+        index2 = int(2 * num_train / fold_k)
+        index3 = int(3 * num_train / fold_k)
+        if Z is None:
+            big = k_ff + sigma_noise_sq * torch.eye(num_train)
+            dss = ns["dss"]
+        else:
+            inducing_x = T(Z).clone().requires_grad_(True)
+            Q_ff = ns["Q"](train_x, inducing_x, train_x)
+            G = (torch.diag(k_ff - Q_ff + sigma_noise_sq * torch.eye(num_train))
+                 * torch.eye(num_train)).type(torch.DoubleTensor)
+            big = Q_ff + G
+            dss = ns["dss_k20"]
+        inv_ij = chol_solve(torch.eye(num_train), big)
+        sl = [slice(0, index1), slice(index1, index2), slice(index2, index3),
+              slice(index3, num_train)]
+        inv_y = chol_solve(train_y, big)
+        tot = 0
+        for s_ in sl:
+            kb = inv_ij[s_, s_]
+            yb = train_y[s_]
+            m = yb - chol_solve(torch.eye(index1), kb).mm(inv_y[s_])
+            if obj == "dss":
+                cov = chol_solve(torch.eye(index1), kb)
+                tot = tot + dss(m, cov, index1, yb)
+            else:
+                cov = torch.diag(chol_solve(torch.eye(index1), kb)).view(index1, 1)
+                tot = tot + crps(m, cov, yb)
+        val = tot.mean()
+        if with_grad:
+            val.backward()
+            out[f"grad_{obj}"] = np.concatenate([para_k.grad.numpy().ravel(),
+                                                 para_l.grad.numpy().ravel(),
+                                                 para_noise.grad.numpy().ravel()])
+            if Z is not None:
+                out[f"gradZ_{obj}"] = inducing_x.grad.numpy().copy()
+        out[f"value_{obj}"] = float(val.detach())
+    return out
+
+
 def synth(seed, n, nt, d):
     """SURVEY.md §8(d) synthetic generator."""
     rng = np.random.default_rng(seed)
@@ -394,6 +460,17 @@ def main():
         save(f"fitc_n{n}_m{mm}_d{dd}_iso", X=X, y=y, Xt=Xt, yt=yt, Z=Z, log_sf2=th[0],
              log_ell=np.array([th[1]]), log_sn2=th[2], **o,
              **grads_fitc(ns, X, y, Z, *th))
+
+    # ---- next-2: 4-fold block-LOO DSS / KC (equal folds: the scripts' chol_solve(eye(index1),
+    # k_f) needs n % 4 == 0) ----------------------------------------------------------
+    for n, mm in ((64, 6), (500, 20)):
+        X, y, Xt, yt, rng2 = synth(4000 + n, n, 16, d)
+        th = (0.1, log_ell8, math.log(0.02))
+        Z = X[rng2.choice(n, mm, replace=False)]
+        save(f"block_full_n{n}", X=X, y=y, log_sf2=th[0], log_ell=th[1], log_sn2=th[2],
+             **block_loo_case(ns, X, y, *th))
+        save(f"block_fitc_n{n}_m{mm}", X=X, y=y, Z=Z, log_sf2=th[0], log_ell=th[1],
+             log_sn2=th[2], **block_loo_case(ns, X, y, *th, Z=Z))
 
     tot = 0
     for name, sz in written:

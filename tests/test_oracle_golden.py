@@ -122,3 +122,23 @@ def test_fitc_oracle_gradients_vs_autograd(name, obj):
     assert abs(val - float(g["value_" + obj])) <= 1e-10 * max(1.0, abs(float(g["value_" + obj])))
     assert nrel(grad, g["grad_" + obj]) <= tol
     assert nrel(gZ, g["gradZ_" + obj]) <= tol
+
+
+BLOCK = golden_names("block_")
+
+
+@pytest.mark.parametrize("name", BLOCK)
+@pytest.mark.parametrize("obj", ["dss", "kc"])
+def test_blockloo_oracle_vs_golden(name, obj):
+    """4-fold block-LOO DSS / KC (KF:487-543, K20:523-587, K20:655-720) composed from the
+    reference's own defs: oracle value (full GP and FITC) and the full-GP analytic gradient
+    against autograd."""
+    g = load_golden(name)
+    th, _ = theta_of(g)
+    ref = float(g["value_" + obj])
+    if "Z" in g:
+        val = O.fast_fitc_blockloo(g["X"], g["y"], g["Z"], *th, obj)
+    else:
+        val, grad = O.fast_full_blockloo(g["X"], g["y"], *th, obj, want_grad=True)
+        assert nrel(grad, g["grad_" + obj]) <= 1e-10
+    assert abs(val - ref) <= 1e-11 * max(1.0, abs(ref))
