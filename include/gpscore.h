@@ -158,6 +158,36 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
                   double obj[GPS_N_OBJ], double* grad, double* grad_z);
 int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]);
 
+/* ---- block-LOO objectives -----------------------------
+ * nfold-fold (the scripts use 4) block leave-out predictive from the diagonal blocks of
+ * A⁻¹: fold f = rows [int(f·n/k), int((f+1)·n/k)) (KF:496-499), m_f = y_f − P_f⁻¹α_f,
+ * C_f = P_f⁻¹, P_f = (A⁻¹)_ff.  GPS_BLOCK_DSS: Σ_f dss(m_f, C_f, y_f) (KF:487-543,
+ * K20:523-587, dss KF:103-108); GPS_BLOCK_KC: Σ_f crps(m_f, diag C_f, y_f) (K20:655-720);
+ * GPS_BLOCK_ES: Σ_f ES(m_f, C_f, y_f) (KF:607-663, ES KF:70-101; gps_full_blockloo_es).
+ * value = the sum over folds, fold_values (nfold, may be NULL) the per-fold terms. */
+enum { GPS_BLOCK_DSS = 0, GPS_BLOCK_KC = 1, GPS_BLOCK_ES = 2 };
+/* Full GP, DSS or KC; grad (2 + n_ell, may be NULL) = the `.backward()` at KF:543 in the
+ * reference's parameterisation.  Leaves the factor for gps_full_predict. */
+int gps_full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell, int nfold,
+                      int objective, double* value, double* grad, double* fold_values);
+/* Full GP, energy score with num_sim draws per fold (300 at KF:652-655) and exponent beta
+ * (1 at KF:70).  draws (2·num_sim·n doubles) hold, fold after fold, ξ_f then ξ'_f
+ * (num_sim × b_f, row-major): the two torch.randn(num_sim, shape1) calls of ES (KF:79-80) in
+ * the scripts' order.  C_f^½ (an SVD at KF:74-77) is the coupled Newton–Schulz iteration on
+ * the MFMA GEMM.  grad as gps_full_blockloo (the `.backward()` at KF:663). */
+int gps_full_blockloo_es(gps_ctx* ctx, int kind, const double* theta, int n_ell, int nfold,
+                         int num_sim, double beta, const double* draws, double* value,
+                         double* grad, double* fold_values);
+/* FITC, DSS or KC; grad (2 + n_ell) and grad_z (m×d, row-major) may be NULL: the
+ * `.backward()` at K20:587 / K20:720 w.r.t. theta and the inducing inputs, which the scripts
+ * move too (K20:593, 726).  All rows on one rank (no communicator). */
+int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, int objective,
+                      double* value, double* grad, double* grad_z, double* fold_values);
+/* ES(m, c, shape1, data_y, num_sim, beta) (KF:70-101) of one Gaussian N(m, C) (b×b,
+ * row-major) at y with the draws given (ξ then ξ', num_sim × b each): the compat helper. */
+int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, const double* y,
+                     int num_sim, double beta, const double* draws, double* out);
+
 /* ---- multi-GPU (RCCL over xGMI) ------------------------------------------- */
 int gps_comm_unique_id(char uid[128]);
 int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]);

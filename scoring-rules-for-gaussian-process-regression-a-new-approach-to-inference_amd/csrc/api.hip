@@ -104,6 +104,10 @@ struct gps_ctx {
   DBuf fX, fy, fXt, fyt, Z, Kmm, Am, Lm, Lb, ldm, ldb, Knm, q, lam, ilam, ys, slabB, red, c, tvec,
       r, g, fmu_loo, fvar_loo, Ksm, qm, qb, fmu, fvar, fslab;
   DBuf fgv, fgm, fgB, fR, fgred, fgslab, fgout;  // FITC gradient scratch
+  // block-LOO scratch (per fold, reused): P, its L⁻¹ / P⁻¹ / H, vectors; full-GP Gblk, T;
+  // FITC gradient: the fold's G_f, E_f, G_fE_f and F = Gblk E; energy score: work area, draws
+  DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
+  size_t bL_zeroed = 0;
   size_t lm_zeroed = 0, lb_zeroed = 0;
   int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
   int fd = 0;
@@ -478,6 +482,254 @@ int bind(gps_ctx* ctx) {
     return -1;
   }
   HIPCHK(hipSetDevice(ctx->device));
+  return 0;
+}
+
+// ------------------------------------------------------------------ block-LOO (next-2)
+// Folds [a_f, b_f) with a_f = int(f·n/k) (KF:496-499).  getP(f, a, b, P, ldp) writes the
+// lower tiles of P_f (b_pad×b_pad, padded as diag(P_f, I)).  Per fold: potrf_inv(P_f) →
+// Lp⁻¹, t = Lp⁻¹α_f, r = P_f⁻¹α_f and c = diag(P_f⁻¹) in one colred pass; then
+//   DSS_f = ½b log2π − ½log|P_f| + ½α_fᵀr,  KC_f = crps(y_f − r, c, y_f),
+//   ES_f  = the energy score of N(y_f − r, P_f⁻¹) at y_f (es_fold).
+// With want_grad, gdst(a, b) names the destination of ∂obj/∂P_f (b×b, symmetric), gdone(f,
+// a, b) runs once it is written, and ∂obj/∂α_f lands in g[a, a+b) (kernels_block.hip).
+std::vector<int64_t> fold_bounds(int64_t n, int nfold) {
+  std::vector<int64_t> bnd(nfold + 1);
+  for (int f = 0; f <= nfold; ++f) bnd[f] = f == nfold ? n : (int64_t)((double)f * n / nfold);
+  return bnd;
+}
+
+// padded edge of the largest fold
+int64_t fold_pad(int64_t n, int nfold) {
+  const std::vector<int64_t> bnd = fold_bounds(n, nfold);
+  int64_t bmax = 1;
+  for (int f = 0; f < nfold; ++f) bmax = std::max(bmax, bnd[f + 1] - bnd[f]);
+  return pad_to(bmax);
+}
+
+struct EsArgs {
+  int S = 0;                      // draws per fold (num_sim: 300 at KF:652-655)
+  double beta = 1.0;              // the score's exponent (KF:70)
+  const double* draws = nullptr;  // device; fold f holds ξ_f then ξ'_f (S×b_f each, row-major)
+  double lam_lb = 0.0;            // λmin(C_f) >= lam_lb; <= 0: unknown, iterate to ‖T − I‖ ≈ 0
+  double diag_ub = 0.0;           // diag(C_f) <= diag_ub, so λmax <= b·diag_ub
+};
+
+// Newton–Schulz steps for a spectrum of C/s inside [x0, 1]: the eigenvalue x of Z_kY_k
+// follows x ← x(3 − x)²/4 (×2.25 per step while small, then quadratic); two more steps let
+// the derivative block of the gradient pass settle
+int ns_iterations(double x0) {
+  double x = std::max(x0, 1e-300);
+  int k = 0;
+  while (1.0 - x > 1e-16 && k < 200) {
+    x = x * (3.0 - x) * (3.0 - x) / 4.0;
+    ++k;
+  }
+  return k + 2;
+}
+
+// Energy score of one fold, ES(m, c, shape1, y, S, β) (KF:70-101) as the scripts call it on
+// the block-LOO predictive (KF:652-655): m − y = −r, C = P_f⁻¹ (PI, full, bp×bp).
+//   R = C^½ by the coupled Newton–Schulz iteration on C/s (T = (3I − ZY)/2, Y ← YT, Z ← TZ:
+//   three b×b MFMA GEMMs per step; the scripts take an SVD, KF:74-77, which has no GEMM form);
+//   z = ξR, ẑ = [ξ'R; −r], D_ij = ‖z_i − ẑ_j‖ (es_dist),
+//   ES = (1/S)Σ_i D_iS^β − Σ_{i,j<S} D_ij^β / (2S(S−1)) (es_reduce) → *out (device).
+// With G (ldg): Ḡ = ∂ES/∂R = ξᵀG_z + ξ'ᵀG_ẑ, G_z = diag(ΣW)z − Wẑ, G_ẑ = diag(ΣWᵀ)ẑ − Wᵀz
+// (W = ∂ES/∂D ∘ D⁻¹); X with RX + XR = sym Ḡ is the off-diagonal block of the same iteration
+// run on [[C, Ḡ], [0, C]] (whose square root is [[R, X], [0, R]]); with w = C·∂ES/∂r:
+//   G = ∂ES/∂P_f = −CXC − ½(wrᵀ + rwᵀ),  g = ∂ES/∂α_f = w.
+int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int64_t bp,
+            const double* PI, const double* r, double trace_c, double* w, double* G, int64_t ldg,
+            double* g, double* out) {
+  hipStream_t s = ctx->stream;
+  const int S = es.S;
+  const int64_t Sp = pad_to(S + 1);
+  const bool grad = G != nullptr;
+  const int nmat = grad ? 10 : 5;
+  const size_t need =
+      (size_t)(6 * Sp * bp + Sp * Sp + 2 * Sp + bp + 8) + (size_t)nmat * bp * bp;
+  HIPCHK(ensure(ctx->ebuf, need * 8));
+  double* q = ctx->ebuf.d();
+  auto take = [&](int64_t cnt) {
+    double* t = q;
+    q += cnt;
+    return t;
+  };
+  double *xi = take(Sp * bp), *xip = take(Sp * bp), *Zs = take(Sp * bp), *Zh = take(Sp * bp);
+  double *Gz = take(Sp * bp), *Gh = take(Sp * bp), *D = take(Sp * Sp), *rsum = take(Sp),
+         *csum = take(Sp), *dr = take(bp), *res = take(8);
+  double* M[10] = {nullptr};
+  for (int i = 0; i < nmat; ++i) M[i] = take(bp * bp);
+  int rc;
+  // C = alpha·op(A)·B + beta·C with N = bp, ldc = bp (every product here has that shape)
+  auto mm = [&](int al, const double* A, int64_t lda, const double* B, double* C, int64_t rows,
+                int64_t kdim, double alpha, double beta) {
+    GemmParams p = gp0();
+    p.A = A; p.lda = lda; p.B = B; p.ldb = bp; p.C = C; p.ldc = bp;
+    p.M = (int)rows; p.N = (int)bp; p.K = (int)kdim; p.alpha = alpha; p.beta = beta;
+    return gemm(ctx, al, LAY_N, EPI_STORE, p);
+  };
+  auto sq = [&](const double* A, const double* B, double* C, double alpha, double beta) {
+    return mm(LAY_N, A, bp, B, C, bp, bp, alpha, beta);
+  };
+  HIPCHK(launch_pad_copy(xi_src, b, xi, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
+  HIPCHK(launch_pad_copy(xi_src + (int64_t)S * b, b, xip, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
+  const bool bounded = es.lam_lb > 0.0;
+  const double sc = bounded ? (double)b * es.diag_ub : trace_c;
+  const int iters = bounded ? ns_iterations(es.lam_lb / sc) : 200;
+  double *Y = M[0], *Z = M[1], *T = M[2], *Yn = M[3], *Zn = M[4];
+  HIPCHK(launch_ns_init(PI, bp, (int)b, (int)bp, 1.0 / sc, 1.0, Y, s));
+  HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 1.0, 1.0, Z, s));
+  int used = 0, extra = -1;
+  for (int it = 0; it < iters; ++it) {
+    if ((rc = sq(Z, Y, T, -0.5, 0.0))) return rc;
+    HIPCHK(launch_diag_add_const(T, bp, (int)bp, 1.5, s));
+    if (!bounded && extra < 0) {  // ‖T − I‖²_F = ‖I − ZY‖²_F / 4
+      HIPCHK(launch_ns_resid(T, bp, (int)bp, res, s));
+      HIPCHK(hipMemcpyAsync(ctx->hsmall, res, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (ctx->hsmall[0] < 1e-24 * (double)bp) extra = 2;
+    }
+    if ((rc = sq(Y, T, Yn, 1.0, 0.0))) return rc;
+    if ((rc = sq(T, Z, Zn, 1.0, 0.0))) return rc;
+    std::swap(Y, Yn);
+    std::swap(Z, Zn);
+    ++used;
+    if (extra >= 0 && extra-- == 0) break;
+  }
+  ARGCHK(bounded || extra >= 0, "energy score: C^1/2 did not converge (is C positive definite?)");
+  const double rt = std::sqrt(sc);
+  if ((rc = mm(LAY_N, xi, bp, Y, Zs, Sp, bp, rt, 0.0))) return rc;
+  if ((rc = mm(LAY_N, xip, bp, Y, Zh, Sp, bp, rt, 0.0))) return rc;
+  HIPCHK(launch_scaled_row(r, (int)b, (int)bp, -1.0, Zh + (int64_t)S * bp, s));
+  HIPCHK(launch_es_dist(Zs, Zh, bp, S, (int)bp, D, Sp, s));
+  HIPCHK(launch_es_reduce(D, Sp, S, (int)Sp, es.beta, grad ? 1 : 0, rsum, csum, out, s));
+  if (!grad) return 0;
+  // G_z = diag(ΣW) z − W ẑ,  G_ẑ = diag(ΣWᵀ) ẑ − Wᵀ z   (W overwrote D, zero-padded)
+  if ((rc = mm(LAY_N, D, Sp, Zh, Gz, Sp, Sp, -1.0, 0.0))) return rc;
+  HIPCHK(launch_row_axpy(Gz, bp, Zs, bp, rsum, (int)Sp, (int)bp, s));
+  if ((rc = mm(LAY_T, D, Sp, Zs, Gh, Sp, Sp, -1.0, 0.0))) return rc;
+  HIPCHK(launch_row_axpy(Gh, bp, Zh, bp, csum, (int)Sp, (int)bp, s));
+  // ∂ES/∂r = −G_ẑ[S] (ẑ_S = −r);  w = C ∂ES/∂r
+  HIPCHK(launch_scaled_row(Gh + (int64_t)S * bp, (int)b, (int)bp, -1.0, dr, s));
+  HIPCHK(launch_gemv_full(PI, bp, dr, w, (int)bp, (int)bp, s));
+  // Ḡ = ξᵀG_z + ξ'ᵀG_ẑ (ξ' is zero from row S on), symmetrised
+  double* Gb = M[5];
+  if ((rc = mm(LAY_T, xi, bp, Gz, Gb, bp, Sp, 1.0, 0.0))) return rc;
+  if ((rc = mm(LAY_T, xip, bp, Gh, Gb, bp, Sp, 1.0, 1.0))) return rc;
+  HIPCHK(launch_sym_avg(Gb, bp, (int)bp, s));
+  // the iteration on [[C, Ḡ], [0, C]]/s: diagonal blocks (Y1, Z1, T1), off-diagonal (Y2, Z2, T2)
+  double *Y1 = M[0], *Z1 = M[1], *T1 = M[2], *Y1n = M[3], *Z1n = M[4], *Z2n = M[5],
+         *Y2 = M[6], *Z2 = M[7], *T2 = M[8], *Y2n = M[9];
+  HIPCHK(launch_ns_init(Gb, bp, (int)b, (int)bp, 1.0 / sc, 0.0, Y2, s));  // before Z2n reuses Gb
+  HIPCHK(launch_ns_init(PI, bp, (int)b, (int)bp, 1.0 / sc, 1.0, Y1, s));
+  HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 1.0, 1.0, Z1, s));
+  HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 0.0, 0.0, Z2, s));
+  for (int it = 0; it < used; ++it) {
+    if ((rc = sq(Z1, Y1, T1, -0.5, 0.0))) return rc;
+    HIPCHK(launch_diag_add_const(T1, bp, (int)bp, 1.5, s));
+    if ((rc = sq(Z1, Y2, T2, -0.5, 0.0))) return rc;
+    if ((rc = sq(Z2, Y1, T2, -0.5, 1.0))) return rc;
+    if ((rc = sq(Y1, T1, Y1n, 1.0, 0.0))) return rc;
+    if ((rc = sq(Y1, T2, Y2n, 1.0, 0.0))) return rc;
+    if ((rc = sq(Y2, T1, Y2n, 1.0, 1.0))) return rc;
+    if ((rc = sq(T1, Z1, Z1n, 1.0, 0.0))) return rc;
+    if ((rc = sq(T1, Z2, Z2n, 1.0, 0.0))) return rc;
+    if ((rc = sq(T2, Z1, Z2n, 1.0, 1.0))) return rc;
+    std::swap(Y1, Y1n);
+    std::swap(Y2, Y2n);
+    std::swap(Z1, Z1n);
+    std::swap(Z2, Z2n);
+  }
+  // X = √s·Y2;  H = C X C (into T1);  G, g by fold_grad
+  if ((rc = sq(Y2, PI, T2, rt, 0.0))) return rc;
+  if ((rc = sq(PI, T2, T1, 1.0, 0.0))) return rc;
+  HIPCHK(launch_fold_grad(PI, bp, T1, bp, r, w, (int)b, 0.0, 0.0, -1.0, -1.0, 0.0, 1.0, G, ldg,
+                          g, s));
+  return 0;
+}
+
+template <class GetP, class GDst, class GDone>
+int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const double* alpha,
+                   const double* y, GetP getP, bool want_grad, GDst gdst, GDone gdone, double* g,
+                   const EsArgs* es, double* vals) {
+  hipStream_t s = ctx->stream;
+  const std::vector<int64_t> bnd = fold_bounds(n, nfold);
+  const int64_t bp = fold_pad(n, nfold);
+  HIPCHK(ensure(ctx->bP, (size_t)bp * bp * 8));
+  if (ctx->bL.cap < (size_t)bp * bp * 8 || ctx->bL_zeroed != (size_t)bp) {
+    HIPCHK(ensure(ctx->bL, (size_t)bp * bp * 8));
+    HIPCHK(hipMemsetAsync(ctx->bL.p, 0, (size_t)bp * bp * 8, s));
+    ctx->bL_zeroed = (size_t)bp;
+  }
+  HIPCHK(ensure(ctx->bPI, (size_t)bp * bp * 8));
+  HIPCHK(ensure(ctx->bH, (size_t)bp * bp * 8));
+  HIPCHK(ensure(ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(bp) * 8)));
+  HIPCHK(ensure(ctx->bvec, (size_t)(9 * bp + 3 * nfold + 8) * 8));
+  const int64_t nchunk = (bp + 255) / 256;
+  HIPCHK(ensure(ctx->slab, std::max(ctx->slab.cap, (size_t)nchunk * bp * 2 * 8)));
+  double* v = ctx->bvec.d();
+  double *ld = v, *af = v + bp, *t = v + 2 * bp, *r = v + 3 * bp, *c = v + 4 * bp,
+         *gm = v + 5 * bp, *gc = v + 6 * bp, *w = v + 7 * bp, *yf = v + 8 * bp;
+  double* fs = v + 9 * bp;  // per fold: [Σ log L_ii, α·r, kc / es]
+  const bool kc = objective == GPS_BLOCK_KC, esq = objective == GPS_BLOCK_ES;
+  int rc;
+  // no reset_info here: a non-PD minor of the caller's main factor must still be reported
+  HIPCHK(hipMemsetAsync(v, 0, (size_t)9 * bp * 8, s));
+  for (int f = 0; f < nfold; ++f) {
+    const int64_t a = bnd[f], b = bnd[f + 1] - bnd[f];
+    if ((rc = getP(f, a, b, ctx->bP.d(), bp))) return rc;
+    if ((rc = potrf_inv(ctx, ctx->bP.d(), bp, ctx->bL.d(), ctx->W.d(), ld, (int)b, nullptr)))
+      return rc;
+    HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
+    HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
+    HIPCHK(launch_gemv_lower(ctx->bL.d(), bp, af, t, (int)bp, s));
+    HIPCHK(launch_colred(ctx->bL.d(), bp, (int)bp, (int)bp, 1, t, nullptr, r, c, ctx->slab.d(), s));
+    HIPCHK(launch_dot(ld, nullptr, (int)b, fs + 3 * f, s));
+    HIPCHK(launch_dot(af, r, (int)b, fs + 3 * f + 1, s));
+    if (kc)
+      HIPCHK(launch_fold_terms(yf, r, c, (int)b, want_grad ? gm : nullptr, gc, fs + 3 * f + 2, s));
+    if (!want_grad && !esq) continue;
+    {  // C_f = P⁻¹ = Lp⁻ᵀLp⁻¹ (full)
+      GemmParams p = gp0();
+      p.A = ctx->bL.d(); p.lda = bp; p.B = ctx->bL.d(); p.ldb = bp; p.C = ctx->bPI.d(); p.ldc = bp;
+      p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.tri = TRI_K_GE_I; p.lower_out = 1;
+      if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+      HIPCHK(launch_sym_mirror(ctx->bPI.d(), bp, (int)bp, s));
+    }
+    double* G = nullptr;
+    int64_t ldg = 0;
+    if (want_grad) {
+      const std::pair<double*, int64_t> dst = gdst(a, b);
+      G = dst.first;
+      ldg = dst.second;
+    }
+    if (esq) {
+      if ((rc = es_fold(ctx, *es, es->draws + 2 * (int64_t)es->S * a, b, bp, ctx->bPI.d(), r, 0.0,
+                        w, G, ldg, want_grad ? g + a : nullptr, fs + 3 * f + 2)))
+        return rc;
+    } else if (!kc) {  // DSS: G_f = −½(P⁻¹ + r rᵀ), g_f = r
+      HIPCHK(launch_fold_grad(ctx->bPI.d(), bp, nullptr, 0, r, nullptr, (int)b, -0.5, -0.5, 0.0,
+                              0.0, 1.0, 0.0, G, ldg, g + a, s));
+    } else {  // KC: w = P⁻¹gm, G_f = ½(w rᵀ + r wᵀ) − P⁻¹diag(gc)P⁻¹, g_f = −w
+      HIPCHK(launch_gemv_full(ctx->bPI.d(), bp, gm, w, (int)bp, (int)bp, s));
+      GemmParams p = gp0();
+      p.A = ctx->bPI.d(); p.lda = bp; p.B = ctx->bPI.d(); p.ldb = bp; p.C = ctx->bH.d();
+      p.ldc = bp; p.kscale = gc; p.M = (int)bp; p.N = (int)bp; p.K = (int)bp;
+      if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
+      HIPCHK(launch_fold_grad(ctx->bPI.d(), bp, ctx->bH.d(), bp, r, w, (int)b, 0.0, 0.0, 1.0,
+                              -1.0, 0.0, -1.0, G, ldg, g + a, s));
+    }
+    if (want_grad && (rc = gdone(f, a, b))) return rc;
+  }
+  std::vector<double> h((size_t)3 * nfold);
+  HIPCHK(hipMemcpyAsync(h.data(), fs, h.size() * 8, hipMemcpyDeviceToHost, s));
+  if ((rc = check_info(ctx))) return rc;
+  for (int f = 0; f < nfold; ++f) {
+    const double b = (double)(bnd[f + 1] - bnd[f]);
+    vals[f] = (kc || esq) ? h[3 * f + 2]
+                          : 0.5 * b * 1.83787706640934548356 - h[3 * f] + 0.5 * h[3 * f + 1];
+  }
   return 0;
 }
 
@@ -1433,6 +1685,422 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   }
   if (n_ell == 1) grad[1] = tot;
   grad[1 + n_ell] = th.sn2 * sum_md;
+  if (grad_z) {
+    const double* z1 = h1 + passes * 17;
+    const double* z2 = h2 + passes * 17;
+    for (int64_t j = 0; j < m; ++j)
+      for (int k = 0; k < d; ++k)
+        grad_z[j * d + k] = (z1[j * d + k] + 2.0 * z2[j * d + k]) * th.inv_ell[k];
+  }
+  return 0;
+}
+
+// 4-fold (nfold) block-LOO objective of the full GP at theta (DSS: KF:487-543; KC: the
+// K20:655-720 body on A = K + σ²I; ES: KF:607-663) and, with grad != NULL, its analytic
+// gradient (`.backward()` at KF:543 / 663): M = −A⁻¹ Gblk A⁻¹ − ½(vαᵀ + αvᵀ), v = A⁻¹g.
+static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell, int nfold,
+                         int objective, const EsArgs* es, double* value, double* grad,
+                         double* fold_values) {
+  int rc;
+  if ((rc = full_fit_core(ctx, kind, theta, n_ell))) return rc;
+  ctx->fitted = true;
+  const int64_t n = ctx->n, np = ctx->n_pad;
+  ARGCHK(n >= nfold, "fewer rows than folds");
+  hipStream_t s = ctx->stream;
+  {  // A⁻¹ (full) = L⁻ᵀL⁻¹ into A
+    GemmParams p = gp0();
+    p.A = ctx->Linv.d(); p.lda = np; p.B = ctx->Linv.d(); p.ldb = np;
+    p.C = ctx->A.d(); p.ldc = np;
+    p.M = (int)np; p.N = (int)np; p.K = (int)np; p.tri = TRI_K_GE_I; p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+    Prof pr(ctx, "grad_mirror", 0, 16.0 * (double)np * np / 2);
+    HIPCHK(launch_sym_mirror(ctx->A.d(), np, (int)np, s));
+  }
+  double* Ainv = ctx->A.d();
+  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bp) -> int {
+    HIPCHK(launch_pad_copy(Ainv + a * np + a, np, P, bp, (int)b, (int)b, (int)bp, (int)bp, 1, s));
+    return 0;
+  };
+  double* Gblk = nullptr;
+  if (grad) {  // zero outside the fold squares (which move with n and nfold): cleared per call
+    HIPCHK(ensure(ctx->bGblk, (size_t)np * np * 8));
+    HIPCHK(hipMemsetAsync(ctx->bGblk.p, 0, (size_t)np * np * 8, s));
+    HIPCHK(ensure(ctx->gu, np * 8));
+    HIPCHK(hipMemsetAsync(ctx->gu.p, 0, np * 8, s));
+    Gblk = ctx->bGblk.d();
+  }
+  auto gdst = [&](int64_t a, int64_t) { return std::make_pair(Gblk + a * np + a, np); };
+  auto gdone = [](int, int64_t, int64_t) { return 0; };
+  std::vector<double> fv(nfold);
+  if ((rc = blockloo_folds(ctx, n, nfold, objective, ctx->alpha.d(), ctx->y.d(), getP,
+                           grad != nullptr, gdst, gdone, grad ? ctx->gu.d() : nullptr, es,
+                           fv.data())))
+    return rc;
+  double tot = 0.0;
+  for (int f = 0; f < nfold; ++f) tot += fv[f];
+  *value = tot;
+  if (fold_values)
+    for (int f = 0; f < nfold; ++f) fold_values[f] = fv[f];
+  if (!grad) return 0;
+  const int d = ctx->d;
+  HIPCHK(ensure(ctx->gv, np * 8));
+  HIPCHK(ensure(ctx->Mx, (size_t)np * np * 8));
+  HIPCHK(ensure(ctx->bT, (size_t)np * np * 8));
+  HIPCHK(launch_gemv_full(Ainv, np, ctx->gu.d(), ctx->gv.d(), (int)np, (int)np, s));
+  {  // T = A⁻¹ Gblk, K restricted per 16-column group to the folds those columns touch
+    const std::vector<int64_t> bnd = fold_bounds(n, nfold);
+    const int64_t groups = np / 16;
+    std::vector<int> kr((size_t)2 * groups, 0);
+    auto fold_of = [&](int64_t col) {
+      int f = 0;
+      while (f + 1 < nfold && col >= bnd[f + 1]) ++f;
+      return f;
+    };
+    for (int64_t q = 0; q < groups; ++q) {
+      const int64_t c0 = q * 16, c1 = std::min<int64_t>(c0 + 15, n - 1);
+      if (c0 >= n) {  // padded columns of Gblk are zero: any range is exact; repeating the
+        kr[2 * q] = kr[2 * q - 2];  // last real group's keeps kr monotone, which the GEMM's
+        kr[2 * q + 1] = kr[2 * q - 1];  // first-group begin / last-group end per tile relies on
+        continue;
+      }
+      kr[2 * q] = (int)(bnd[fold_of(c0)] / 16 * 16);
+      kr[2 * q + 1] = (int)std::min<int64_t>(np, (bnd[fold_of(c1) + 1] + 15) / 16 * 16);
+    }
+    HIPCHK(ensure(ctx->bkr, kr.size() * sizeof(int)));
+    HIPCHK(hipMemcpyAsync(ctx->bkr.p, kr.data(), kr.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    GemmParams p = gp0();
+    p.A = Ainv; p.lda = np; p.B = Gblk; p.ldb = np; p.C = ctx->bT.d(); p.ldc = np;
+    p.M = (int)np; p.N = (int)np; p.K = (int)np; p.tri = TRI_KR_J;
+    p.kr = static_cast<const int*>(ctx->bkr.p);
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
+    HIPCHK(hipStreamSynchronize(s));  // the host kr vector must outlive the async copy
+  }
+  {  // Mx = T A⁻¹ (lower tiles)
+    GemmParams p = gp0();
+    p.A = ctx->bT.d(); p.lda = np; p.B = Ainv; p.ldb = np; p.C = ctx->Mx.d(); p.ldc = np;
+    p.M = (int)np; p.N = (int)np; p.K = (int)np; p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
+  }
+  GradParams gpar;
+  memset(&gpar, 0, sizeof(gpar));
+  gpar.x = ctx->X.d(); gpar.n = (int)n; gpar.d = d; gpar.sf2 = ctx->th.sf2;
+  for (int k = 0; k < d; ++k) gpar.inv_ell[k] = ctx->th.inv_ell[k];
+  gpar.Ainv = Ainv; gpar.ldm = np; gpar.alpha = ctx->alpha.d();
+  gpar.a2 = -1.0; gpar.a3 = -1.0; gpar.v = ctx->gv.d(); gpar.Mx = ctx->Mx.d();
+  const int passes = grad_contract_passes(d);
+  HIPCHK(ensure(ctx->gslab, (size_t)grad_contract_slab_doubles((int)n, d) * 8));
+  HIPCHK(ensure(ctx->gout, (size_t)passes * 18 * 8));
+  gpar.slab = ctx->gslab.d();
+  {
+    Prof pr(ctx, "grad_contract", 0, 16.0 * (double)n * n / 2);
+    HIPCHK(launch_grad_contract(gpar, ctx->gout.d(), s));
+  }
+  std::vector<double> hout((size_t)passes * 18);
+  HIPCHK(hipMemcpyAsync(hout.data(), ctx->gout.p, hout.size() * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const double bscale = kind == GPS_RBF ? 0.5 : 1.0;
+  grad[0] = hout[0];
+  double gl = 0.0;
+  for (int k = 0; k < d; ++k) {
+    const double gk = bscale * hout[(size_t)(k / 16) * 18 + 2 + (k % 16)];
+    if (n_ell == d) grad[1 + k] = gk;
+    gl += gk;
+  }
+  if (n_ell == 1) grad[1] = gl;
+  grad[1 + n_ell] = ctx->th.sn2 * hout[1];
+  return 0;
+}
+
+int gps_full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell, int nfold,
+                      int objective, double* value, double* grad, double* fold_values) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(nfold >= 1 && nfold <= 64, "nfold must be in 1..64");
+  ARGCHK(objective == GPS_BLOCK_DSS || objective == GPS_BLOCK_KC,
+         "objective must be GPS_BLOCK_DSS or GPS_BLOCK_KC (the energy score: gps_full_blockloo_es)");
+  ARGCHK(value != nullptr, "value is NULL");
+  return full_blockloo(ctx, kind, theta, n_ell, nfold, objective, nullptr, value, grad,
+                       fold_values);
+}
+
+// Energy-score block-LOO objective of the full GP (KF:607-663) with the caller's draws.
+// C_f = ((A⁻¹)_ff)⁻¹ is a conditional covariance (Schur complement of A = K + σ²I), so
+// σ²I <= C_f and diag C_f <= sf2 + σ²: these fix the Newton–Schulz scale and step count.
+int gps_full_blockloo_es(gps_ctx* ctx, int kind, const double* theta, int n_ell, int nfold,
+                         int num_sim, double beta, const double* draws, double* value,
+                         double* grad, double* fold_values) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(nfold >= 1 && nfold <= 64, "nfold must be in 1..64");
+  ARGCHK(num_sim >= 2 && num_sim <= 8192, "num_sim must be in 2..8192");
+  ARGCHK(beta > 0.0 && beta <= 2.0, "beta must be in (0, 2]");
+  ARGCHK(theta && draws && value, "NULL argument");
+  ARGCHK(ctx->have_data, "gps_full_set_data first");
+  ARGCHK(n_ell == 1 || n_ell == ctx->d, "n_ell must be 1 or d");
+  const int64_t cnt = 2 * (int64_t)num_sim * ctx->n;
+  HIPCHK(ensure(ctx->edraws, (size_t)cnt * 8));
+  HIPCHK(hipMemcpyAsync(ctx->edraws.p, draws, (size_t)cnt * 8, hipMemcpyHostToDevice, ctx->stream));
+  EsArgs es;
+  es.S = num_sim;
+  es.beta = beta;
+  es.draws = ctx->edraws.d();
+  es.lam_lb = std::exp(theta[1 + n_ell]);
+  es.diag_ub = std::exp(theta[0]) + es.lam_lb;
+  return full_blockloo(ctx, kind, theta, n_ell, nfold, GPS_BLOCK_ES, &es, value, grad,
+                       fold_values);
+}
+
+// ES(m, c, shape1, data_y, num_sim, beta) (KF:70-101) of one Gaussian N(m, C) at y with the
+// draws given (ξ then ξ', num_sim × b each): the compat helper.  No spectral bounds are known
+// for a general C, so the Newton–Schulz iteration runs on C/trace(C) until ‖I − ZY‖ ≈ 0.
+int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, const double* y,
+                     int num_sim, double beta, const double* draws, double* out) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(m && C && y && draws && out && b >= 1 && b <= (1 << 16), "bad argument");
+  ARGCHK(num_sim >= 2 && num_sim <= 8192, "num_sim must be in 2..8192");
+  ARGCHK(beta > 0.0 && beta <= 2.0, "beta must be in (0, 2]");
+  hipStream_t s = ctx->stream;
+  const int64_t bp = pad_to(b);
+  if (int rc = upload(ctx, ctx->t0, C, b, b, b)) return rc;
+  HIPCHK(ensure(ctx->bPI, (size_t)bp * bp * 8));
+  HIPCHK(launch_pad_copy(ctx->t0.d(), b, ctx->bPI.d(), bp, (int)b, (int)b, (int)bp, (int)bp, 1, s));
+  std::vector<double> r(b);  // the residual y − m (input marshalling: ẑ_S = m − y = −r)
+  double tr = 0.0;
+  for (int64_t i = 0; i < b; ++i) {
+    r[i] = y[i] - m[i];
+    tr += C[i * b + i];
+  }
+  ARGCHK(tr > 0.0, "C must be positive definite");
+  if (int rc = upload(ctx, ctx->t1, r.data(), b, 1, bp)) return rc;
+  HIPCHK(ensure(ctx->t2, (size_t)bp * 8));
+  const int64_t cnt = 2 * (int64_t)num_sim * b;
+  HIPCHK(ensure(ctx->edraws, (size_t)cnt * 8));
+  HIPCHK(hipMemcpyAsync(ctx->edraws.p, draws, (size_t)cnt * 8, hipMemcpyHostToDevice, s));
+  EsArgs es;
+  es.S = num_sim;
+  es.beta = beta;
+  es.draws = ctx->edraws.d();
+  double* dev_out = ctx->small.d();
+  if (int rc = es_fold(ctx, es, es.draws, b, bp, ctx->bPI.d(), ctx->t1.d(), tr, ctx->t2.d(),
+                       nullptr, 0, nullptr, dev_out))
+    return rc;
+  HIPCHK(hipMemcpyAsync(ctx->hsmall, dev_out, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *out = ctx->hsmall[0];
+  return 0;
+}
+
+// FITC block-LOO objective (K20:523-587 DSS, K20:655-720 KC): P_f = ((Q+Λ)⁻¹)_ff =
+// Λ_f⁻¹ − U_fU_fᵀ with U = Λ⁻¹K Lb⁻ᵀ (one n×m TRMM), α = (y − Kc)/λ.  With grad / grad_z the
+// `.backward()` at K20:587 / 720 w.r.t. θ and the inducing inputs (moved at K20:593 / 726):
+// M = −C⁻¹GblkC⁻¹ − ½(vαᵀ + αvᵀ), v = C⁻¹g (C = Q + Λ); Woodbury with E = Λ⁻¹KB⁻¹ = C⁻¹KKm⁻¹:
+//   F = Gblk E (one b×b×m GEMM per fold), S = EᵀF, T = KᵀΛ⁻¹F (n·m² each),
+//   G_K  = −2Λ⁻¹F + 2Λ⁻¹K(B⁻¹T) − 2diag(M_ii)KKm⁻¹ − vcᵀ − αŵᵀ,  ŵ = Km⁻¹Kᵀv,
+//   G_Km = S + Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹ + ½(ŵcᵀ + cŵᵀ),
+//   M_ii = −(G_ii − 2F_i·K_i + (KS)_i·K_i)/λ_i² − v_iα_i   (blk_mdiag, kernels_block.hip),
+// contracted with ∂K/∂θ, ∂K/∂Z like gps_fitc_grad.  All rows on one rank.
+int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, int objective,
+                      double* value, double* grad, double* grad_z, double* fold_values) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(nfold >= 1 && nfold <= 64, "nfold must be in 1..64");
+  ARGCHK(objective == GPS_BLOCK_DSS || objective == GPS_BLOCK_KC,
+         "objective must be GPS_BLOCK_DSS or GPS_BLOCK_KC");
+  ARGCHK(value != nullptr, "value is NULL");
+  ARGCHK(ctx->comm == nullptr, "FITC block-LOO needs every row on one rank");
+  double o[GPS_N_OBJ];
+  int rc;
+  if ((rc = fitc_fit_core(ctx, theta, n_ell, o))) return rc;
+  ctx->f_fitted = true;
+  const Theta& th = ctx->fth;
+  const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
+  const int d = ctx->fd;
+  ARGCHK(n >= nfold, "fewer rows than folds");
+  hipStream_t s = ctx->stream;
+  const bool want = grad != nullptr || grad_z != nullptr;
+  const int64_t ldr = want ? 3 * mp : mp;  // [U | E | K Km⁻¹]; U's slot later holds KS, KB⁻¹T
+  const int64_t bp = fold_pad(n, nfold);
+  HIPCHK(ensure(ctx->fR, (size_t)np * ldr * 8));
+  HIPCHK(ensure(ctx->fgv, (size_t)13 * np * 8));
+  double* U = ctx->fR.d();
+  double* E = U + mp;
+  double* RC = U + 2 * mp;
+  double* vb = ctx->fgv.d();
+  double *alpha = vb, *dinv = vb + np, *v = vb + 2 * np, *ulam = vb + 3 * np, *hh = vb + 4 * np,
+         *hl2 = vb + 5 * np, *gg = vb + 6 * np, *gd = vb + 7 * np, *md = vb + 8 * np,
+         *sa = vb + 9 * np, *sb = vb + 10 * np, *scl = vb + 11 * np, *zv = vb + 12 * np;
+  HIPCHK(launch_fitc_grad_terms(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n, (int)np,
+                                GPS_OBJ_NLML, (double)n, alpha, dinv, v, ulam, hh, hl2, s));
+  {  // U = Λ⁻¹ K Lb⁻ᵀ
+    GemmParams p = gp0();
+    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp; p.C = U; p.ldc = ldr;
+    p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
+    HIPCHK(launch_row_scale(U, ldr, (int)np, (int)mp, ctx->ilam.d(), s));
+  }
+  auto gemm_nn = [&](const double* A, int64_t lda, const double* B, double* C, int64_t ldc,
+                     int64_t rows) -> int {
+    GemmParams p = gp0();
+    p.A = A; p.lda = lda; p.B = B; p.ldb = mp; p.C = C; p.ldc = ldc;
+    p.M = (int)rows; p.N = (int)mp; p.K = (int)mp;
+    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
+  };
+  double *Binv = nullptr, *Kminv = nullptr, *Sm = nullptr, *Tm = nullptr, *BT = nullptr,
+         *KmD = nullptr, *F = nullptr;
+  if (want) {
+    HIPCHK(ensure(ctx->fgB, (size_t)6 * mp * mp * 8));
+    double* Bb = ctx->fgB.d();
+    Binv = Bb; Kminv = Bb + mp * mp; Sm = Bb + 2 * mp * mp; Tm = Bb + 3 * mp * mp;
+    BT = Bb + 4 * mp * mp; KmD = Bb + 5 * mp * mp;
+    const double* Ls[2] = {ctx->Lb.d(), ctx->Lm.d()};
+    double* Is[2] = {Binv, Kminv};
+    for (int q = 0; q < 2; ++q) {  // B⁻¹, Km⁻¹ (LAUUM, lower tiles) + mirror
+      GemmParams p = gp0();
+      p.A = Ls[q]; p.lda = mp; p.B = Ls[q]; p.ldb = mp; p.C = Is[q]; p.ldc = mp;
+      p.M = (int)mp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_I; p.lower_out = 1;
+      if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+      HIPCHK(launch_sym_mirror(Is[q], mp, (int)mp, s));
+    }
+    if ((rc = gemm_nn(ctx->Knm.d(), mp, Binv, E, ldr, np))) return rc;  // E = Λ⁻¹ K B⁻¹
+    HIPCHK(launch_row_scale(E, ldr, (int)np, (int)mp, ctx->ilam.d(), s));
+    HIPCHK(ensure(ctx->bF, (size_t)np * mp * 8));
+    HIPCHK(ensure(ctx->bEf, (size_t)bp * mp * 8));
+    HIPCHK(ensure(ctx->bFf, (size_t)bp * mp * 8));
+    HIPCHK(ensure(ctx->bG, (size_t)bp * bp * 8));
+    HIPCHK(hipMemsetAsync(ctx->bG.p, 0, (size_t)bp * bp * 8, s));
+    F = ctx->bF.d();
+    HIPCHK(hipMemsetAsync(F, 0, (size_t)np * mp * 8, s));
+    HIPCHK(hipMemsetAsync(gg, 0, (size_t)2 * np * 8, s));  // g and diag(Gblk)
+  }
+  HIPCHK(ensure(ctx->bT, (size_t)bp * mp * 8));
+  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bpp) -> int {
+    double* Uf = ctx->bT.d();
+    HIPCHK(launch_pad_copy(U + a * ldr, ldr, Uf, mp, (int)b, (int)mp, (int)bpp, (int)mp, 0, s));
+    GemmParams p = gp0();
+    p.A = Uf; p.lda = mp; p.B = Uf; p.ldb = mp; p.C = P; p.ldc = bpp;
+    p.M = (int)bpp; p.N = (int)bpp; p.K = (int)mp; p.alpha = -1.0; p.lower_out = 1;
+    if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
+    HIPCHK(launch_add_diag(P, bpp, ctx->ilam.d() + a, (int)b, (int)bpp, s));
+    return 0;
+  };
+  auto gdst = [&](int64_t, int64_t) { return std::make_pair(ctx->bG.d(), bp); };
+  auto gdone = [&](int, int64_t a, int64_t b) -> int {  // F rows of the fold = G_f E_f; diag G_f
+    double* Ef = ctx->bEf.d();
+    double* Ff = ctx->bFf.d();
+    HIPCHK(launch_pad_copy(E + a * ldr, ldr, Ef, mp, (int)b, (int)mp, (int)bp, (int)mp, 0, s));
+    GemmParams p = gp0();
+    p.A = ctx->bG.d(); p.lda = bp; p.B = Ef; p.ldb = mp; p.C = Ff; p.ldc = mp;
+    p.M = (int)bp; p.N = (int)mp; p.K = (int)bp;
+    if (int rc2 = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p)) return rc2;
+    HIPCHK(launch_pad_copy(Ff, mp, F + a * mp, mp, (int)b, (int)mp, (int)b, (int)mp, 0, s));
+    HIPCHK(launch_pad_copy(ctx->bG.d(), bp + 1, gd + a, 1, (int)b, 1, (int)b, 1, 0, s));
+    return 0;
+  };
+  std::vector<double> fv(nfold);
+  if ((rc = blockloo_folds(ctx, n, nfold, objective, alpha, ctx->fy.d(), getP, want, gdst, gdone,
+                           want ? gg : nullptr, nullptr, fv.data())))
+    return rc;
+  double tot = 0.0;
+  for (int f = 0; f < nfold; ++f) tot += fv[f];
+  *value = tot;
+  if (fold_values)
+    for (int f = 0; f < nfold; ++f) fold_values[f] = fv[f];
+  if (!want) return 0;
+  // v = C⁻¹g = g/λ − Λ⁻¹K B⁻¹Kᵀ(g/λ)
+  HIPCHK(ensure(ctx->fgm, (size_t)6 * mp * 8));
+  double* mb = ctx->fgm.d();
+  double *tku = mb, *tbt = mb + mp, *what = mb + 2 * mp;
+  HIPCHK(launch_vec_mul(gg, ctx->ilam.d(), (int)np, ulam, s));
+  HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr,
+                       ctx->fslab.d(), s));
+  HIPCHK(launch_gemv_full(Binv, mp, tku, tbt, (int)mp, (int)mp, s));
+  HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, tbt, zv, (int)np, (int)mp, s));
+  HIPCHK(launch_fitc_grad_v(ulam, zv, ctx->lam.d(), (int)n, v, s));
+  {  // T = KᵀΛ⁻¹F, S = EᵀF (m×m, n·m² each)
+    GemmParams p = gp0();
+    p.A = ctx->Knm.d(); p.lda = mp; p.B = F; p.ldb = mp; p.C = Tm; p.ldc = mp;
+    p.kscale = ctx->ilam.d(); p.M = (int)mp; p.N = (int)mp; p.K = (int)np;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+    GemmParams q = gp0();
+    q.A = E; q.lda = ldr; q.B = F; q.ldb = mp; q.C = Sm; q.ldc = mp;
+    q.M = (int)mp; q.N = (int)mp; q.K = (int)np;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, q))) return rc;
+  }
+  if ((rc = gemm_nn(Binv, mp, Tm, BT, mp, mp))) return rc;          // B⁻¹T
+  if ((rc = gemm_nn(ctx->Knm.d(), mp, Sm, U, ldr, np))) return rc;  // K S (into U's slot)
+  {
+    Prof pr(ctx, "blk_mdiag", 0, 24.0 * np * mp);
+    HIPCHK(launch_blk_mdiag(F, mp, U, ldr, ctx->Knm.d(), mp, (int)mp, gd, ctx->lam.d(), v, alpha,
+                            (int)n, (int)np, md, sa, sb, scl, s));
+  }
+  if ((rc = gemm_nn(ctx->Knm.d(), mp, BT, U, ldr, np))) return rc;      // K B⁻¹T
+  if ((rc = gemm_nn(ctx->Knm.d(), mp, Kminv, RC, ldr, np))) return rc;  // K Km⁻¹
+  // ŵ = Km⁻¹Kᵀv;  Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹;  Σ M_ii
+  HIPCHK(ensure(ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
+  double* red = ctx->fgred.d();
+  double* tw = red + mp * mp;
+  double* smd = red + mp * mp + mp;
+  HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, v, nullptr, tw, nullptr,
+                       ctx->fslab.d(), s));
+  HIPCHK(launch_gemv_full(Kminv, mp, tw, what, (int)mp, (int)mp, s));
+  if ((rc = fitc_syrk(ctx, md, nullptr, red))) return rc;
+  HIPCHK(launch_dot(md, nullptr, (int)np, smd, s));
+  HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
+  if ((rc = gemm_nn(red, mp, Kminv, Tm, mp, mp))) return rc;
+  if ((rc = gemm_nn(Kminv, mp, Tm, KmD, mp, mp))) return rc;
+  // contractions with ∂Knm/∂θ, ∂Knm/∂Z and ∂Kmm/∂θ, ∂Kmm/∂Z
+  const int passes = fitc_contract_passes(d);
+  const int64_t outlen = (int64_t)passes * 17 + m * d;
+  HIPCHK(ensure(ctx->fgslab, (size_t)std::max(fitc_contract_slab_doubles((int)n, (int)mp, d),
+                                               fitc_contract_slab_doubles((int)m, (int)mp, d)) * 8));
+  HIPCHK(ensure(ctx->fgout, (size_t)(2 * outlen + 8) * 8));
+  double* out1 = ctx->fgout.d();
+  double* out2 = out1 + outlen;
+  FitcContractParams cp;
+  memset(&cp, 0, sizeof(cp));
+  cp.d = d;
+  cp.sf2 = th.sf2;
+  for (int k = 0; k < d; ++k) cp.inv_ell[k] = th.inv_ell[k];
+  cp.slab = ctx->fgslab.d();
+  {
+    FitcContractParams p = cp;
+    p.xr = ctx->fX.d(); p.xc = ctx->Z.d(); p.nr = (int)n; p.nc = (int)m; p.nc_pad = (int)mp;
+    p.R[0] = F; p.ldr[0] = mp; p.coef[0] = 1.0; p.rs[0] = sa;
+    p.R[1] = U; p.ldr[1] = ldr; p.coef[1] = 1.0; p.rs[1] = sb;
+    p.R[2] = RC; p.ldr[2] = ldr; p.coef[2] = 1.0; p.rs[2] = scl;
+    p.nt = 3;
+    p.pc[0] = -1.0; p.pv[0] = v; p.qv[0] = ctx->c.d();
+    p.pc[1] = -1.0; p.pv[1] = alpha; p.qv[1] = what;
+    Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * 3 * np * mp);
+    HIPCHK(launch_fitc_grad_contract(p, out1, out1 + passes * 17, s));
+  }
+  {
+    FitcContractParams p = cp;
+    p.xr = ctx->Z.d(); p.xc = ctx->Z.d(); p.nr = (int)m; p.nc = (int)m; p.nc_pad = (int)mp;
+    p.R[0] = Sm; p.ldr[0] = mp; p.coef[0] = 1.0;
+    p.R[1] = KmD; p.ldr[1] = mp; p.coef[1] = 1.0;
+    p.nt = 2;
+    p.pc[0] = 0.5; p.pv[0] = what; p.qv[0] = ctx->c.d();
+    p.pc[1] = 0.5; p.pv[1] = ctx->c.d(); p.qv[1] = what;
+    Prof pr(ctx, "fitc_grad_contract_mm", 0, 8.0 * 2 * mp * mp);
+    HIPCHK(launch_fitc_grad_contract(p, out2, out2 + passes * 17, s));
+  }
+  std::vector<double> hout((size_t)2 * outlen + 1);
+  HIPCHK(hipMemcpyAsync(hout.data(), out1, (size_t)2 * outlen * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hout.data() + 2 * outlen, smd, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const double* h1 = hout.data();
+  const double* h2 = h1 + outlen;
+  const double sum_md = hout[2 * outlen];
+  if (grad) {
+    grad[0] = h1[0] + h2[0] + th.sf2 * sum_md;
+    double gl = 0.0;
+    for (int k = 0; k < d; ++k) {
+      const size_t at = (size_t)(k / 16) * 17 + 1 + (k % 16);
+      const double gk = h1[at] + h2[at];
+      if (n_ell == d) grad[1 + k] = gk;
+      gl += gk;
+    }
+    if (n_ell == 1) grad[1] = gl;
+    grad[1 + n_ell] = th.sn2 * sum_md;
+  }
   if (grad_z) {
     const double* z1 = h1 + passes * 17;
     const double* z2 = h2 + passes * 17;

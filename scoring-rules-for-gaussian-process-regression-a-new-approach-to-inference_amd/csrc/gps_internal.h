@@ -41,6 +41,8 @@ enum Tri {
   TRI_K_LE_J = 2,  // k < (tj+1)*128   (B = Lᵀ with L lower stored [j][k])
   TRI_K_GE_J = 3,  // k >= tj*128      (B lower stored [k][j])
   TRI_K_GE_I = 4,  // k >= ti*128      (A = Lᵀ with L lower stored [k][i])
+  TRI_KR_J = 5,    // k in [kr[2g], kr[2g'+1]) over the 16-column groups g..g' of the tile
+                   // (B block-diagonal with unaligned blocks: block-LOO gradients)
 };
 enum Epi { EPI_STORE = 0, EPI_ROWSQ = 1, EPI_COLRED = 2 };
 
@@ -57,6 +59,7 @@ struct GemmParams {
   int lower_out;             // enumerate only tiles with tj <= ti
   int ksplit;                // number of K slices (grid.y)
   int tri;
+  const int* kr;             // TRI_KR_J: per 16-column group [k begin, k end) (multiples of 16)
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
                              // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto
@@ -205,6 +208,39 @@ int grad_contract_passes(int d);
 int64_t grad_contract_slab_doubles(int n, int d);
 // out[pass*18 + q]: q = 0 Σ w m K, 1 Σ_diag m, 2+k Σ w m K Δ²_(16·pass+k)
 hipError_t launch_grad_contract(const GradParams& p, double* out, hipStream_t s);
+
+// --- block-LOO (kernels_block.hip)
+hipError_t launch_fold_terms(const double* y, const double* r, const double* c, int b, double* gm,
+                             double* gc, double* out, hipStream_t s);
+hipError_t launch_fold_grad(const double* PI, int64_t ldp, const double* H, int64_t ldh,
+                            const double* r, const double* w, int b, double c0, double c1,
+                            double c2, double c3, double gr, double gw, double* G, int64_t ldg,
+                            double* g, hipStream_t s);
+hipError_t launch_add_diag(double* P, int64_t ld, const double* vals, int nreal, int npad,
+                           hipStream_t s);
+hipError_t launch_row_scale(double* M, int64_t ld, int rows, int cols, const double* scale,
+                            hipStream_t s);
+hipError_t launch_vec_mul(const double* a, const double* b, int n, double* out, hipStream_t s);
+// FITC block-LOO gradient: M_ii and the row scales of G_K (see kernels_block.hip)
+hipError_t launch_blk_mdiag(const double* F, int64_t ldf, const double* KS, int64_t ldks,
+                            const double* K, int64_t ldk, int m_pad, const double* gd,
+                            const double* lam, const double* v, const double* alpha, int n,
+                            int n_pad, double* md, double* sa, double* sb, double* sc,
+                            hipStream_t s);
+// energy score: Newton–Schulz steps, distances, reduction
+hipError_t launch_ns_init(const double* C, int64_t ldc, int b, int bp, double scale, double pad,
+                          double* Y, hipStream_t s);
+hipError_t launch_diag_add_const(double* M, int64_t ld, int n, double c, hipStream_t s);
+hipError_t launch_sym_avg(double* M, int64_t ld, int n, hipStream_t s);
+hipError_t launch_scaled_row(const double* src, int b, int bp, double scale, double* dst,
+                             hipStream_t s);
+hipError_t launch_row_axpy(double* C, int64_t ldc, const double* Z, int64_t ldz, const double* sv,
+                           int rows, int cols, hipStream_t s);
+hipError_t launch_ns_resid(const double* T, int64_t ld, int n, double* out, hipStream_t s);
+hipError_t launch_es_dist(const double* Z, const double* Zh, int64_t ld, int S, int bp, double* D,
+                          int64_t ldd, hipStream_t s);
+hipError_t launch_es_reduce(double* D, int64_t ldd, int S, int Sp, double beta, int grad,
+                            double* rs, double* cs, double* out, hipStream_t s);
 
 // --- FITC gradients (kernels_fitc_grad.hip)
 hipError_t launch_fitc_grad_terms(const double* y, const double* lam, const double* r,

@@ -136,6 +136,10 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     case TRI_K_LE_J: ke = min(ke, col0 + TILE); break;
     case TRI_K_GE_J: kb = col0; break;
     case TRI_K_GE_I: kb = row0; break;
+    case TRI_KR_J:
+      kb = p.kr[2 * (col0 / 16)];
+      ke = p.kr[2 * ((col0 + TILE) / 16 - 1) + 1];
+      break;
     default: break;
   }
   if (p.ksplit > 1) {
@@ -400,6 +404,10 @@ __global__ __launch_bounds__(256) void gemm_f64_tiny_kernel(GemmParams p) {
     case TRI_K_LE_J: ke = min(ke, col0 + 16); break;
     case TRI_K_GE_J: kb = col0; break;
     case TRI_K_GE_I: kb = row0; break;
+    case TRI_KR_J:
+      kb = p.kr[2 * (col0 / 16)];
+      ke = p.kr[2 * (col0 / 16) + 1];
+      break;
     default: break;
   }
   const int r = lane & 15, g = lane >> 4;
@@ -549,10 +557,10 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   int tiles = (int)tiles_for(q, tile);
   // triangular operands default to the XCD-banded heaviest-first order (map 3):
   // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build
-  if (q.map_mode == 0 && q.tri != TRI_NONE && !q.lower_out) q.map_mode = 3;
+  if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out) q.map_mode = 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
   if (q.map_mode == 3) {
-    if (q.lower_out || q.tri == TRI_NONE) return hipErrorInvalidValue;
+    if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
                                                           : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;
   }

@@ -56,6 +56,11 @@ SIGNATURES = {
     "gps_fitc_set_inducing": (_c_int, [_c_vp, _P, _c_i64]),
     "gps_fitc_fit": (_c_int, [_c_vp, _P, _c_int, _P, _P, _P]),
     "gps_fitc_grad": (_c_int, [_c_vp, _P, _c_int, _c_int, _P, _P, _P]),
+    "gps_full_blockloo": (_c_int, [_c_vp, _c_int, _P, _c_int, _c_int, _c_int, _P, _P, _P]),
+    "gps_full_blockloo_es": (_c_int, [_c_vp, _c_int, _P, _c_int, _c_int, _c_int, _c_dbl, _P, _P,
+                                      _P, _P]),
+    "gps_fitc_blockloo": (_c_int, [_c_vp, _P, _c_int, _c_int, _c_int, _P, _P, _P, _P]),
+    "gps_energy_score": (_c_int, [_c_vp, _P, _P, _c_i64, _P, _c_int, _c_dbl, _P, _P]),
     "gps_fitc_predict": (_c_int, [_c_vp, _P, _P, _P]),
     "gps_comm_unique_id": (_c_int, [_c_cp]),
     "gps_comm_init": (_c_int, [_c_vp, _c_int, _c_int, _c_cp]),

@@ -21,6 +21,19 @@ import numpy as np
 from . import _lib
 from ._lib import GPS_ARD, GPS_RBF, OBJ_NAMES, SCORE_NAMES, f64, ptr
 
+BLOCK_OBJS = ["dss", "kc", "es"]  # GPS_BLOCK_DSS, GPS_BLOCK_KC, GPS_BLOCK_ES
+
+
+def es_draws(n, nfold=4, num_sim=300, rng=None):
+    """Standard-normal draws of the block-LOO energy score in the C-ABI's layout: fold f (rows
+    [int(f·n/k), int((f+1)·n/k)), KF:496-499) holds ξ_f then ξ'_f, each num_sim × b_f — the
+    two torch.randn(num_sim, shape1) calls of ES (KF:79-80) in the scripts' fold order.
+    ``rng``: a numpy Generator, a seed, or None (fresh entropy, as the scripts re-draw)."""
+    rng = np.random.default_rng(rng)
+    bnd = [0] + [int(f * n / nfold) for f in range(1, nfold)] + [n]
+    return np.concatenate([rng.standard_normal(2 * num_sim * (b - a))
+                           for a, b in zip(bnd[:-1], bnd[1:])])
+
 
 def pack_theta(theta, d):
     """[log_sf2, log_ell..., log_sn2] as the C-ABI expects; returns (array, n_ell)."""
@@ -133,19 +146,28 @@ class GP:
         return FitResult(self.kind, dict(zip(OBJ_NAMES, obj.tolist())), mu, var)
 
     # ------------------------------------------------------------- gradients
-    def value_and_grad(self, theta, objective="loo_crps", X=None, y=None, rbf=False, Z=None):
+    def value_and_grad(self, theta, objective="loo_crps", X=None, y=None, rbf=False, Z=None,
+                       **block_kw):
         """Objective value and its analytic gradient at theta — the forward body plus the
         `.backward()` of one GD iteration of the reference (full GP: KF:239-252 LOO-CRPS,
-        KF:329-339 NLML, KF:416-428 LOO-LogS; FITC: K20:222-236, 329-344, 434-452).
+        KF:329-339 NLML, KF:416-428 LOO-LogS, KF:487-543 DSS, KF:607-663 ES; FITC:
+        K20:222-236, 329-344, 434-452, 523-587 DSS, 655-720 KC).
         Returns (value, grad, objectives) with grad = [d/d para_k, d/d para_l (1 or d),
         d/d para_noise]; for FITC ``objectives["grad_Z"]`` holds d/d inducing_x (m×d),
-        the inducing inputs being trained parameters there (K20:247)."""
+        the inducing inputs being trained parameters there (K20:247).  ``block_kw`` goes to
+        block_loo (nfold, num_sim, beta, draws, rng)."""
         if X is not None:
             self.set_data(X, y, kind="fitc" if Z is not None else "full", Z=Z)
         elif Z is not None:
             self.set_inducing(Z)
+        if objective in BLOCK_OBJS:
+            res = self.block_loo(theta, objective, grad=True, rbf=rbf, **block_kw)
+            objs = {objective: res[0], "folds": res[2]}
+            if self.kind == "fitc":
+                objs["grad_Z"] = res[3]
+            return res[0], res[1], objs
         if objective not in OBJ_NAMES[:3]:
-            raise ValueError(f"objective must be one of {OBJ_NAMES[:3]}")
+            raise ValueError(f"objective must be one of {OBJ_NAMES[:3] + BLOCK_OBJS}")
         th, n_ell = pack_theta(theta, self._X.shape[1])
         obj = np.zeros(5)
         grad = np.zeros(2 + n_ell)
@@ -165,8 +187,48 @@ class GP:
         objs = dict(zip(OBJ_NAMES, obj.tolist()))
         return objs[objective], grad, objs
 
+    def block_loo(self, theta, objective="dss", nfold=4, grad=False, rbf=False, num_sim=300,
+                  beta=1.0, draws=None, rng=None):
+        """k-fold block leave-out objective at theta, summed over the
+        folds as the scripts do: "dss" — the Dawid-Sebastiani score of each fold's block-LOO
+        predictive (full GP KF:487-543, FITC K20:523-587); "kc" — the fold-mean CRPS of its
+        marginals (K20:655-720); "es" — the energy score of the fold's multivariate predictive
+        (full GP, ES KF:70-101 in the loop KF:607-663) from num_sim draws per fold: pass
+        ``draws`` (es_draws layout) to fix them, else they are drawn from ``rng`` (the scripts
+        re-draw torch.randn on every call).
+        Returns value, or with grad=True (value, grad, per-fold values) — the `.backward()` at
+        KF:543 / 663 — and for FITC also d/d inducing_x: (value, grad, folds, grad_Z)."""
+        if objective not in BLOCK_OBJS:
+            raise ValueError(f"objective must be one of {BLOCK_OBJS}")
+        n, d = self._X.shape
+        th, n_ell = pack_theta(theta, d)
+        val = np.zeros(1)
+        folds = np.zeros(nfold)
+        code = BLOCK_OBJS.index(objective)
+        g = np.zeros(2 + n_ell) if grad else None
+        if self.kind == "fitc":
+            if objective == "es":
+                raise ValueError("the energy score is a full-GP objective (KF:607-663)")
+            gz = np.zeros_like(self._Z) if grad else None
+            self.ctx.call("gps_fitc_blockloo", ptr(th), n_ell, nfold, code, ptr(val), ptr(g),
+                          ptr(gz), ptr(folds))
+            return (float(val[0]), g, folds, gz) if grad else float(val[0])
+        kind = GPS_RBF if rbf else GPS_ARD
+        if objective == "es":
+            if draws is None:
+                draws = es_draws(n, nfold, num_sim, rng)
+            draws = f64(draws).ravel()
+            if draws.size != 2 * num_sim * n:
+                raise ValueError(f"draws must hold 2·num_sim·n = {2 * num_sim * n} values")
+            self.ctx.call("gps_full_blockloo_es", kind, ptr(th), n_ell, nfold, int(num_sim),
+                          float(beta), ptr(draws), ptr(val), ptr(g), ptr(folds))
+        else:
+            self.ctx.call("gps_full_blockloo", kind, ptr(th), n_ell, nfold, code, ptr(val), ptr(g),
+                          ptr(folds))
+        return (float(val[0]), g, folds) if grad else float(val[0])
+
     def train(self, theta0, objective="loo_crps", lr=1.0, itr=400, X=None, y=None, rbf=False,
-              callback=None, Z0=None, lr_z=None):
+              callback=None, Z0=None, lr_z=None, block_kw=None):
         """The reference's GD fit loop: `itr` plain SGD steps para -= lr * grad on
         (para_k, para_l, para_noise) — full GP e.g. KF:236-260 — one forward + analytic
         backward per step on the device.  FITC (K20:219-251, 324-354, 428-458) also moves
@@ -188,7 +250,7 @@ class GP:
         params = np.zeros((itr, th.size))
         for i in range(itr):
             val, g, objs = self.value_and_grad((th[0], th[1:1 + n_ell], th[-1]), objective,
-                                               rbf=rbf)
+                                               rbf=rbf, **(block_kw or {}))
             values[i] = val
             th -= lr * g
             params[i] = th

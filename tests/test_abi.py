@@ -21,7 +21,7 @@ def header_symbols():
 def test_header_declares_core_entry_points():
     syms = header_symbols()
     for s in ("gps_gram", "gps_potrf", "gps_potrs", "gps_diag_inv", "gps_full_fit",
-              "gps_full_predict", "gps_scores", "gps_fitc_fit", "gps_fitc_grad", "gps_fitc_predict",
+              "gps_full_predict", "gps_scores", "gps_fitc_fit", "gps_fitc_grad", "gps_fitc_predict", "gps_full_blockloo", "gps_fitc_blockloo",
               "gps_comm_init", "gps_ctx_create", "gps_last_error"):
         assert s in syms
 
