@@ -13,6 +13,8 @@ SIMPLE-DATA FULL-comapre.py (SD):
     crps(m, c, data_y) / logs(m, c, data_y)            KF:60-68 / KF:52-57
     trivial_loss(m, c, data_y, data_yp)                KF:110-119
     SMSE(m, data_y, data_yp)                           KF:128-134
+    dss(m, c, shape1, data_y)                          KF:103-108
+    ES(m, c, shape1, data_y, num_sim=300, beta=1)      KF:70-101  (draws: see ES)
 
 The reference reads module globals ``para_k``, ``para_l``, ``sigma_noise_sq``
 and ``dtype``; here they live on ``compat.state`` (settable attributes with the
@@ -199,6 +201,36 @@ def SMSE(m, data_y, data_yp):
     """MSE / MSE of the train-mean predictor (KF:128-134)."""
     m = f64(_np(m)).ravel()
     return float(_scores(m, np.ones_like(m), data_y, data_yp)[3])
+
+
+def dss(m, c, shape1, data_y):
+    """Dawid–Sebastiani score of N(m, c) at data_y (KF:103-108; K20:106-111 inverts c instead of
+    solving, the same number): ½·shape1·log2π + ½log|c| + ½(y − m)ᵀc⁻¹(y − m)."""
+    C = f64(_np(c), 2)
+    r = (f64(_np(data_y)).ravel() - f64(_np(m)).ravel()).reshape(-1, 1)
+    quad = float(mm(r, chol_solve(r, C), transA=True)[0, 0])
+    return 0.5 * int(shape1) * LOG2PI + half_logdet(C) + 0.5 * quad
+
+
+def ES(m, c, shape1, data_y, num_sim=300, beta=1, draws=None, rng=None):
+    """Energy score of N(m, c) at data_y from num_sim draws (KF:70-101):
+    (1/S)Σ_i ‖z_i − (m − y)‖^β − Σ_ij ‖z_i − z'_j‖^β / (2S(S−1)),  z = ξc^½, z' = ξ'c^½.
+    ``draws`` (2·num_sim·shape1 values: ξ then ξ', row-major) fixes ξ, ξ'; the reference
+    draws them with torch.randn on every call — here from ``rng`` (numpy) when not given."""
+    C = f64(_np(c), 2)
+    b = C.shape[0]
+    if int(shape1) != b:
+        raise ValueError("shape1 must be c's order (the draws are num_sim × shape1, KF:79)")
+    mv, yv = f64(_np(m)).ravel(), f64(_np(data_y)).ravel()
+    if draws is None:
+        draws = np.random.default_rng(rng).standard_normal(2 * int(num_sim) * b)
+    draws = f64(draws).ravel()
+    if draws.size != 2 * int(num_sim) * b:
+        raise ValueError("draws must hold 2·num_sim·shape1 values")
+    out = np.zeros(1)
+    _ctx().call("gps_energy_score", ptr(mv), ptr(C), b, ptr(yv), int(num_sim), float(beta),
+                ptr(draws), ptr(out))
+    return float(out[0])
 
 
 LOG2PI = math.log(2.0 * math.pi)

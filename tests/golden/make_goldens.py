@@ -40,7 +40,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 # four scripts; rbf exists only in SD/SF)
 SOURCES = {
     "kin40k-FULL-compare.py": ["ARD", "chol_solve", "Q", "crps", "logs",
-                               "trivial_loss", "cal_mean_and_cov", "SMSE", "dss"],
+                               "trivial_loss", "cal_mean_and_cov", "SMSE", "dss", "ES"],
     "KIN40K-COMPARE-ALL-FITC-20.py": ["spgp_cal_mean_and_cov"],
     "SIMPLE-DATA FULL-comapre.py": ["rbf"],
 }
@@ -330,6 +330,47 @@ def block_loo_case(ns, X, y, log_sf2, log_ell, log_sn2, Z=None, with_grad=True):
     return out
 
 
+def es_case(ns, X, y, log_sf2, log_ell, log_sn2, num_sim, seed):
+    """4-fold block-LOO energy score composed as the ES loop writes it (KF:615-663; ES
+    KF:70-101 through the extracted def): value, autograd gradient, and the standard-normal
+    draws its torch.randn calls consumed — the same seed replayed, fold by fold ξ then ξ'
+    (KF:79-80), in the layout the C-ABI takes."""
+    para_k = T([log_sf2]).requires_grad_(True)
+    para_l = T(np.atleast_1d(log_ell)).view(1, -1).clone().requires_grad_(True)
+    para_noise = T([log_sn2]).requires_grad_(True)
+    ns["para_k"], ns["para_l"], ns["dtype"] = para_k, para_l, torch.DoubleTensor
+    train_x, train_y = T(X), T(y).view(-1, 1)
+    num_train = train_x.shape[0]
+    chol_solve = ns["chol_solve"]
+    sigma_noise_sq = torch.exp(para_noise)                                    # KF:618
+    k_ff = ns["ARD"](train_x, train_x, para_k, para_l)                        # KF:619
+    fold_k = 4
+    index1 = int(num_train / fold_k)
+    index2 = int(2 * num_train / fold_k)
+    index3 = int(3 * num_train / fold_k)
+    big_k = k_ff + sigma_noise_sq * torch.eye(num_train)                      # KF:625
+    k_inv_i_j = chol_solve(torch.eye(num_train), big_k)                       # KF:626
+    k_inv_y = chol_solve(train_y, big_k)                                       # KF:638
+    sl = [slice(0, index1), slice(index1, index2), slice(index2, index3),
+          slice(index3, num_train)]
+    torch.manual_seed(seed)
+    tot = 0
+    for s_ in sl:
+        kb = k_inv_i_j[s_, s_]
+        yb = train_y[s_]
+        m = yb - chol_solve(torch.eye(index1), kb).mm(k_inv_y[s_])             # KF:640-643
+        cov = chol_solve(torch.eye(index1), kb)                                # KF:646-649
+        tot = tot + ns["ES"](m, cov, index1, yb, num_sim)                      # KF:652-655
+    val = tot.mean()                                                           # KF:657
+    val.backward()                                                             # KF:663
+    torch.manual_seed(seed)
+    draws = np.concatenate([torch.randn(num_sim, index1).numpy().ravel() for _ in range(2 * fold_k)])
+    return {"value_es": float(val.detach()),
+            "grad_es": np.concatenate([para_k.grad.numpy().ravel(), para_l.grad.numpy().ravel(),
+                                       para_noise.grad.numpy().ravel()]),
+            "draws_es": draws, "num_sim": num_sim}
+
+
 def synth(seed, n, nt, d):
     """SURVEY.md §8(d) synthetic generator."""
     rng = np.random.default_rng(seed)
@@ -359,12 +400,15 @@ def simple_data(ns, seed):
     return X, y, Xt, yt, k_init[:16, :16].numpy()
 
 
-def main():
+def main(only=None):
+    """only: name prefixes to (re)write (all when None); e.g. `make_goldens.py blockes_ es_`."""
     torch.set_default_dtype(torch.float64)
     ns = load_reference_defs()
     written = []
 
     def save(name, **arrs):
+        if only and not any(name.startswith(p) for p in only):
+            return
         path = os.path.join(OUT, name + ".npz")
         np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrs.items()})
         written.append((name, os.path.getsize(path)))
@@ -472,6 +516,28 @@ def main():
         save(f"block_fitc_n{n}_m{mm}", X=X, y=y, Z=Z, log_sf2=th[0], log_ell=th[1],
              log_sn2=th[2], **block_loo_case(ns, X, y, *th, Z=Z))
 
+    # ---- next-2: the energy score (ES KF:70-101) on the 4-fold block-LOO predictive
+    # (KF:607-663), the reference's own torch.randn draws replayed -------------------------
+    for n, S in ((64, 300), (200, 40)):
+        X, y, _, _, _ = synth(5000 + n, n, 16, d)
+        th = (0.1, log_ell8, math.log(0.02))
+        save(f"blockes_full_n{n}", X=X, y=y, log_sf2=th[0], log_ell=th[1], log_sn2=th[2],
+             **es_case(ns, X, y, *th, num_sim=S, seed=7 + n))
+
+    # ---- ES / dss helpers on one fixed Gaussian (compat.ES / compat.dss) -----------------
+    rng = np.random.default_rng(23)
+    b = 12
+    A0 = rng.standard_normal((b, b))
+    C = A0 @ A0.T / b + 0.1 * np.eye(b)
+    m, yv = rng.standard_normal(b), rng.standard_normal(b)
+    with torch.no_grad():
+        torch.manual_seed(5)
+        es1 = float(ns["ES"](T(m).view(-1, 1), T(C), b, T(yv).view(-1, 1), 40))
+        torch.manual_seed(5)
+        dr = np.concatenate([torch.randn(40, b).numpy().ravel() for _ in range(2)])
+        dss1 = float(ns["dss"](T(m).view(-1, 1), T(C), b, T(yv).view(-1, 1)))
+    save("es_single", m=m, C=C, y=yv, num_sim=40, draws=dr, es=es1, dss=dss1)
+
     tot = 0
     for name, sz in written:
         print(f"{name:28s} {sz/1024:8.1f} KiB")
@@ -480,4 +546,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

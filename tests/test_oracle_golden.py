@@ -136,9 +136,39 @@ def test_blockloo_oracle_vs_golden(name, obj):
     g = load_golden(name)
     th, _ = theta_of(g)
     ref = float(g["value_" + obj])
-    if "Z" in g:
-        val = O.fast_fitc_blockloo(g["X"], g["y"], g["Z"], *th, obj)
+    if "Z" in g:  # FITC: θ- and inducing-input gradients (K20:587 / 720, Z moved at K20:593 / 726)
+        val, grad, gZ = O.fast_fitc_blockloo(g["X"], g["y"], g["Z"], *th, obj, want_grad=True)
+        assert nrel(grad, g["grad_" + obj]) <= 1e-10
+        assert nrel(gZ, g["gradZ_" + obj]) <= 1e-10
+        assert abs(O.fast_fitc_blockloo(g["X"], g["y"], g["Z"], *th, obj) - val) <= 1e-13 * abs(val)
     else:
         val, grad = O.fast_full_blockloo(g["X"], g["y"], *th, obj, want_grad=True)
         assert nrel(grad, g["grad_" + obj]) <= 1e-10
     assert abs(val - ref) <= 1e-11 * max(1.0, abs(ref))
+
+
+@pytest.mark.parametrize("name", golden_names("blockes_"))
+def test_es_oracle_vs_golden(name):
+    """4-fold block-LOO energy score (KF:607-663) from the reference's own ES def (KF:70-101)
+    with its torch.randn draws replayed: oracle value, and the analytic gradient (the Sylvester
+    solution RX + XR = Ḡ for d C^½) against autograd through torch.svd."""
+    g = load_golden(name)
+    th, _ = theta_of(g)
+    es = {"draws": g["draws_es"], "S": int(g["num_sim"])}
+    val, grad = O.fast_full_blockloo(g["X"], g["y"], *th, "es", want_grad=True, es=es)
+    ref = float(g["value_es"])
+    assert abs(val - ref) <= 1e-11 * max(1.0, abs(ref))
+    assert nrel(grad, g["grad_es"]) <= 1e-10
+    assert abs(O.fast_full_blockloo(g["X"], g["y"], *th, "es", es=es) - val) <= 1e-13 * abs(val)
+
+
+def test_es_dss_single_oracle_vs_golden():
+    """ES and dss of one Gaussian (KF:70-108) with the reference's draws."""
+    g = load_golden("es_single")
+    S, b = int(g["num_sim"]), g["C"].shape[0]
+    xi = g["draws"].reshape(2, S, b)
+    v = O.es_value(g["m"], g["C"], g["y"], xi[0], xi[1])
+    assert abs(v - float(g["es"])) <= 1e-12 * max(1.0, abs(float(g["es"])))
+    r = g["y"] - g["m"]
+    d = 0.5 * b * O.LOG2PI + 0.5 * np.linalg.slogdet(g["C"])[1] + 0.5 * r @ np.linalg.solve(g["C"], r)
+    assert abs(d - float(g["dss"])) <= 1e-12 * max(1.0, abs(float(g["dss"])))
