@@ -580,24 +580,24 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
   double *Y = M[0], *Z = M[1], *T = M[2], *Yn = M[3], *Zn = M[4];
   HIPCHK(launch_ns_init(PI, bp, (int)b, (int)bp, 1.0 / sc, 1.0, Y, s));
   HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 1.0, 1.0, Z, s));
-  int used = 0, extra = -1;
-  for (int it = 0; it < iters; ++it) {
+  int used = 0, extra = -1;  // adaptive mode: steps still to run once converged
+  for (int it = 0; it < iters && extra != 0; ++it) {
     if ((rc = sq(Z, Y, T, -0.5, 0.0))) return rc;
     HIPCHK(launch_diag_add_const(T, bp, (int)bp, 1.5, s));
     if (!bounded && extra < 0) {  // ‖T − I‖²_F = ‖I − ZY‖²_F / 4
       HIPCHK(launch_ns_resid(T, bp, (int)bp, res, s));
       HIPCHK(hipMemcpyAsync(ctx->hsmall, res, 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
-      if (ctx->hsmall[0] < 1e-24 * (double)bp) extra = 2;
+      if (ctx->hsmall[0] < 1e-24 * (double)bp) extra = 3;
     }
     if ((rc = sq(Y, T, Yn, 1.0, 0.0))) return rc;
     if ((rc = sq(T, Z, Zn, 1.0, 0.0))) return rc;
     std::swap(Y, Yn);
     std::swap(Z, Zn);
     ++used;
-    if (extra >= 0 && extra-- == 0) break;
+    if (extra > 0) --extra;
   }
-  ARGCHK(bounded || extra >= 0, "energy score: C^1/2 did not converge (is C positive definite?)");
+  ARGCHK(bounded || extra == 0, "energy score: C^1/2 did not converge (is C positive definite?)");
   const double rt = std::sqrt(sc);
   if ((rc = mm(LAY_N, xi, bp, Y, Zs, Sp, bp, rt, 0.0))) return rc;
   if ((rc = mm(LAY_N, xip, bp, Y, Zh, Sp, bp, rt, 0.0))) return rc;

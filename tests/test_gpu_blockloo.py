@@ -201,7 +201,10 @@ def test_fitc_blockloo_finite_difference(gp, obj):
     fd = (f(th + h * u, Z + h * uz) - f(th - h * u, Z - h * uz)) / (2 * h)
     an = grad @ u + np.sum(gz * uz)
     scale = max(abs(fd), 1e-3 * np.sqrt(np.sum(grad ** 2) + np.sum(gz ** 2)))
-    assert abs(fd - an) <= 1e-5 * scale, (fd, an)
+    # plus the difference quotient's rounding floor: the objective carries ~1e-13 relative
+    # noise (cond(K̃mm) at m = 200), i.e. ~1e-13·|val|/h here (10× margin); measured: KC's
+    # quotient scatters ±3e-8 around the analytic 5.5e-4 as h changes
+    assert abs(fd - an) <= 1e-5 * scale + 1e-12 * abs(val) / h, (fd, an)
 
 
 def test_fitc_blockloo_sgd_train(gp):
