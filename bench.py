@@ -199,6 +199,7 @@ def main():
     ap.add_argument("--no-fitc", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-grad", action="store_true")
+    ap.add_argument("--no-block", action="store_true", help="skip the block-LOO (next-2) leg")
     ap.add_argument("--lookahead", type=int, default=0,
                     help="recursion depths with a split (lookahead) trailing update; 0 disables")
     ap.add_argument("--reserve-cus", type=int, default=None,
@@ -291,6 +292,28 @@ def main():
                        "(fit + A^-1 + [A^-1 diag(c) A^-1] + dA/dtheta contraction); flop = n^3 "
                        "(NLML) / 2n^3 (LOO) at n_pad", **grad}
 
+    # ---------------- next-2: block-LOO objectives, one GD iteration each (C2) ----------------
+    if not args.no_block:
+        from gpscore.gp import es_draws
+        cb = CONFIGS["C2"]
+        Xb, yb, _, _, _, thb = synth(cb["n"], cb["d"], cb["nt"], cb["seed"])
+        bgp = gpscore.GP(ctx=ctx)
+        bgp.set_data(Xb, yb)
+        draws = es_draws(cb["n"], 4, 300, np.random.default_rng(0))
+        blk = {}
+        for objective in ("dss", "kc", "es"):
+            kw = {"num_sim": 300, "draws": draws} if objective == "es" else {}
+
+            def bstep():
+                return bgp.block_loo(thb, objective, grad=True, **kw)
+            bstep()
+            k = max(1, args.steps // 2)
+            blk[objective] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, bstep, k) / k}
+        res["block_loo"] = {"config": f"C2 full GP n={cb['n']}, 4 folds of {cb['n'] // 4}; ES with "
+                            "300 draws per fold (KF:652-655)",
+                            "note": "value + analytic gradient per GD iteration (KF:487-543, "
+                                    "K20:655-720, KF:607-663)", **blk}
+
     # ---------------- FITC (rows sharded, RCCL all-reduce) ----------------
     if not args.no_fitc:
         from gpscore.dist import shard_rows
@@ -343,6 +366,12 @@ def main():
                     fgstep()
                     k = max(1, args.steps // 2)
                     fg[objective] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, fgstep, k) / k}
+                if leg == "C4" and world == 1 and not args.no_block:  # next-2: K20:655-726 KC
+                    def fbstep():
+                        return fgp.block_loo(thf, "kc", grad=True)
+                    fbstep()
+                    fg["block_kc"] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, fbstep, 1),
+                                      "note": "4 folds of 10 000 rows, theta and Z gradient"}
                 fitc[leg]["grad"] = fg
             del Xf, yf, Xtf, ytf
         if world > 1 and not args.rehearse:
