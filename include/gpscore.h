@@ -81,6 +81,11 @@ enum {
   GPS_OPT_MAIN_CU_EXCLUDE = 6, /* recreate the context's own main stream CU-masked so that the
                              top `value` CU ids (r/8 per XCD) stay free for other streams/
                              contexts (0 = unmasked, the default).  For co-scheduling studies. */
+  GPS_OPT_SYRK_SPLIT = 8,  /* 1: the factorisation's trailing updates with >= one full round
+                             of 128-tiles split K (1..4 slices) to fill the last round of
+                             resident workgroups; 0 (default, measured faster end-to-end on
+                             C3 because the overlap streams already fill it): one launch.  Same numerics up to
+                             the order of the K summation (deterministic either way). */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

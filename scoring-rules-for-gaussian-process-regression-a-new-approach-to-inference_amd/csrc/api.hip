@@ -121,6 +121,8 @@ struct gps_ctx {
   DBuf t0, t1, t2, t3, t4;
   // ---- split-K slabs, one per stream (GEMMs on different streams run concurrently)
   DBuf ws_main, ws_side, ws_look[2];
+  DBuf ws_syrk;                        // split-K slabs of the trailing update (syrk_splits)
+  int syrk_split = 0;                  // GPS_OPT_SYRK_SPLIT: 1 fill-model split-K, 0 off (default: C3 A/B 130.5 vs 129.6 ms)
 };
 
 namespace {
@@ -304,6 +306,26 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
   return 0;
 }
 
+// Split-K of the trailing update A22 −= L21 L21ᵀ.  Its lower 128-tiles all carry the same
+// K, so a grid that is not a whole number of rounds of resident workgroups (2 per CU) idles
+// the last round: 3160 tiles at the C3 top level are 6.17 rounds of 512.  Take ks in 1..4
+// maximising the filled fraction of the last round, 1 % off per extra slice for the slab
+// traffic, keeping >= 512 of K per slice.  tools/gemm_bench syrk (MI355X): 10112², K = 9984
+// 60.2 → 65.4 / 66.7 / 67.2 TF/s at ks 2 / 3 / 4; 5120² 53.5 → 62.4 at ks 3; 4992² 51.5 → 59.8.
+int syrk_splits(int64_t tiles, int slots, int K) {
+  int best = 1;
+  double best_score = 0.0;
+  for (int ks = 1; ks <= 4 && K / ks >= 512; ++ks) {
+    const double x = (double)tiles * ks / slots;
+    const double score = x / std::ceil(x) * (1.0 - 0.01 * (ks - 1));
+    if (score > best_score + 1e-9) {
+      best_score = score;
+      best = ks;
+    }
+  }
+  return best;
+}
+
 // recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
 // W is this level's workspace (n1·n2 doubles); deeper levels on the A22 side get
 // the region after it, so a concurrent GEMM that still reads this level's W never
@@ -364,6 +386,14 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
     p.M = m1; p.N = m1; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
+    const int64_t tiles = (int64_t)(m1 / GPS_TILE) * (m1 / GPS_TILE + 1) / 2;
+    const int ks = ctx->syrk_split && tiles >= 2 * ctx->ncu ? syrk_splits(tiles, 2 * ctx->ncu, n1)
+                                                             : 1;
+    if (ks > 1) {
+      HIPCHK(ensure(ctx->ws_syrk, (size_t)ks * m1 * m1 * 8));
+      p.tile = GPS_TILE; p.ksplit = ks; p.ws = ctx->ws_syrk.d();
+      p.ws_cap = (int64_t)(ctx->ws_syrk.cap / 8);
+    }
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
   }
   if (look) {
@@ -803,7 +833,10 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
                  &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
                  &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_look[0], &ctx->ws_look[1],
-                 &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout};
+                 &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
+                 &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
+                 &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
+                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws, &ctx->ws_syrk};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
@@ -842,6 +875,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
     case GPS_OPT_FUSED_SPLITK: ctx->fused_splitk = value != 0; return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
+    case GPS_OPT_SYRK_SPLIT: ctx->syrk_split = value != 0; return 0;
     case GPS_OPT_MAIN_CU_EXCLUDE: {  // recreate the (owned) main stream CU-masked
       ARGCHK(ctx->own_stream, "the main stream is caller-owned");
       HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -2,7 +2,8 @@
 ~5% in GEMM clocks, so variants must be compared inside one run).
 
   python tools/ab_bench.py --config C3 la=2,map=0 la=0,map=0 la=2,map=4
-  options: la (GPS_OPT_LOOKAHEAD), map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN)
+  options: la (GPS_OPT_LOOKAHEAD), map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN),
+  syrk (GPS_OPT_SYRK_SPLIT)
 Variants are interleaved round-robin for --rounds rounds; prints the median ms/unit.
 """
 import argparse
@@ -21,7 +22,7 @@ import gpscore  # noqa: E402
 from gpscore import _lib  # noqa: E402
 
 KEYS = {"la": _lib.GPS_OPT_LOOKAHEAD, "map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP,
-        "fork": _lib.GPS_OPT_FORK_MIN}
+        "fork": _lib.GPS_OPT_FORK_MIN, "syrk": _lib.GPS_OPT_SYRK_SPLIT}
 
 
 def main():

@@ -116,6 +116,26 @@ static int ldstudy(double* A, double* B, double* C) {
   return 0;
 }
 
+// top-level trailing update of the C3 factorisation (3160 lower 128-tiles = 6.2 rounds of
+// 512 resident workgroups): split-K through slabs vs the single launch
+static int syrk_study(double* A, double* B, double* C) {
+  double* ws;
+  if (hipMalloc(&ws, (int64_t)4 * 10112 * 10112 * 8) != hipSuccess) return 1;
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (int M : {10112, 5120, 4992}) {
+    const int K = M == 10112 ? 9984 : M;
+    const double fl = (double)M * (M + 1) * K;
+    for (int tile : {128, 64})
+      for (int ks : {1, 2, 3, 4}) {
+        p.A = A; p.B = A; p.C = C; p.lda = K; p.ldb = K; p.ldc = M;
+        p.M = M; p.N = M; p.K = K; p.lower_out = 1; p.alpha = -1.0; p.beta = 1.0;
+        p.tile = tile; p.ksplit = ks; p.ws = ks > 1 ? ws : nullptr; p.ws_cap = (int64_t)4 * 10112 * 10112;
+        printf("SYRK M=%5d K=%5d t%3d ks%d %7.2f TF/s\n", M, K, tile, ks, run(LAY_N, LAY_T, EPI_STORE, p, 5, fl));
+      }
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 20480;
   double *A, *B, *C, *o0, *o1, *w;
@@ -130,6 +150,7 @@ int main(int argc, char** argv) {
   hipMemset(w, 0, n * 8);
   printf("operands: %s\n", zeros ? "zeros" : "uniform random [-0.5, 0.5)");
   if (argc > 1 && !strcmp(argv[1], "ld")) return ldstudy(A, B, C);
+  if (argc > 1 && !strcmp(argv[1], "syrk")) return syrk_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "sweep")) {
     double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);
     return sweep(A, B, C, ws);
