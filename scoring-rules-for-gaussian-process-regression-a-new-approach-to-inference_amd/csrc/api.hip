@@ -576,8 +576,16 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
   const int64_t Sp = pad_to(S + 1);
   const bool grad = G != nullptr;
   const int nmat = grad ? 10 : 5;
-  const size_t need =
-      (size_t)(6 * Sp * bp + Sp * Sp + 2 * Sp + bp + 8) + (size_t)nmat * bp * bp;
+  const bool bounded = es.lam_lb > 0.0;
+  const double sc = bounded ? (double)b * es.diag_ub : trace_c;
+  const int iters = bounded ? ns_iterations(es.lam_lb / sc) : 200;
+  // with a gradient and a known step count the forward iterates Y_k, Z_k, T_k are kept
+  // (3·iters + 2 matrices, < 1 GB at b = 1250) so the derivative pass runs only the
+  // 6 products of the off-diagonal blocks per step instead of 9
+  const size_t nstore = grad && bounded ? (size_t)3 * iters + 2 : 0;
+  const bool stored = nstore && nstore * bp * bp * 8 <= ((size_t)16 << 30);
+  const size_t need = (size_t)(6 * Sp * bp + Sp * Sp + 2 * Sp + bp + 8) +
+                      ((size_t)nmat + (stored ? nstore : 0)) * bp * bp;
   HIPCHK(ensure(ctx->ebuf, need * 8));
   double* q = ctx->ebuf.d();
   auto take = [&](int64_t cnt) {
@@ -590,6 +598,12 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
          *csum = take(Sp), *dr = take(bp), *res = take(8);
   double* M[10] = {nullptr};
   for (int i = 0; i < nmat; ++i) M[i] = take(bp * bp);
+  std::vector<double*> Ys, Zk, Ts;  // stored iterates: Y_0..Y_iters, Z_0..Z_iters, T_0..T_iters-1
+  if (stored) {
+    for (int k = 0; k <= iters; ++k) Ys.push_back(take(bp * bp));
+    for (int k = 0; k <= iters; ++k) Zk.push_back(take(bp * bp));
+    for (int k = 0; k < iters; ++k) Ts.push_back(take(bp * bp));
+  }
   int rc;
   // C = alpha·op(A)·B + beta·C with N = bp, ldc = bp (every product here has that shape)
   auto mm = [&](int al, const double* A, int64_t lda, const double* B, double* C, int64_t rows,
@@ -602,26 +616,43 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
   auto sq = [&](const double* A, const double* B, double* C, double alpha, double beta) {
     return mm(LAY_N, A, bp, B, C, bp, bp, alpha, beta);
   };
+  // Every Newton–Schulz iterate is a polynomial in C (Y_k, Z_k, T_k commute), and the
+  // off-diagonal blocks of the gradient pass are Fréchet derivatives of those polynomials
+  // in the symmetric direction Ḡ: every product (or pair sum) below is symmetric, so it
+  // is formed on the lower tiles only (half the flops) and mirrored.
+  auto sym = [&](const double* A, const double* B, double* C, double alpha, double beta) {
+    GemmParams p = gp0();
+    p.A = A; p.lda = bp; p.B = B; p.ldb = bp; p.C = C; p.ldc = bp;
+    p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.alpha = alpha; p.beta = beta; p.lower_out = 1;
+    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
+  };
+  auto mirror = [&](double* C) { return launch_sym_mirror(C, bp, (int)bp, s); };
   HIPCHK(launch_pad_copy(xi_src, b, xi, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
   HIPCHK(launch_pad_copy(xi_src + (int64_t)S * b, b, xip, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
-  const bool bounded = es.lam_lb > 0.0;
-  const double sc = bounded ? (double)b * es.diag_ub : trace_c;
-  const int iters = bounded ? ns_iterations(es.lam_lb / sc) : 200;
-  double *Y = M[0], *Z = M[1], *T = M[2], *Yn = M[3], *Zn = M[4];
+  double *Y = stored ? Ys[0] : M[0], *Z = stored ? Zk[0] : M[1], *T = M[2], *Yn = M[3],
+         *Zn = M[4];
   HIPCHK(launch_ns_init(PI, bp, (int)b, (int)bp, 1.0 / sc, 1.0, Y, s));
   HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 1.0, 1.0, Z, s));
   int used = 0, extra = -1;  // adaptive mode: steps still to run once converged
   for (int it = 0; it < iters && extra != 0; ++it) {
-    if ((rc = sq(Z, Y, T, -0.5, 0.0))) return rc;
+    if (stored) {
+      T = Ts[it];
+      Yn = Ys[it + 1];
+      Zn = Zk[it + 1];
+    }
+    if ((rc = sym(Z, Y, T, -0.5, 0.0))) return rc;
     HIPCHK(launch_diag_add_const(T, bp, (int)bp, 1.5, s));
+    HIPCHK(mirror(T));
     if (!bounded && extra < 0) {  // ‖T − I‖²_F = ‖I − ZY‖²_F / 4
       HIPCHK(launch_ns_resid(T, bp, (int)bp, res, s));
       HIPCHK(hipMemcpyAsync(ctx->hsmall, res, 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       if (ctx->hsmall[0] < 1e-24 * (double)bp) extra = 3;
     }
-    if ((rc = sq(Y, T, Yn, 1.0, 0.0))) return rc;
-    if ((rc = sq(T, Z, Zn, 1.0, 0.0))) return rc;
+    if ((rc = sym(Y, T, Yn, 1.0, 0.0))) return rc;
+    HIPCHK(mirror(Yn));
+    if ((rc = sym(T, Z, Zn, 1.0, 0.0))) return rc;
+    HIPCHK(mirror(Zn));
     std::swap(Y, Yn);
     std::swap(Z, Zn);
     ++used;
@@ -648,29 +679,48 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
   if ((rc = mm(LAY_T, xi, bp, Gz, Gb, bp, Sp, 1.0, 0.0))) return rc;
   if ((rc = mm(LAY_T, xip, bp, Gh, Gb, bp, Sp, 1.0, 1.0))) return rc;
   HIPCHK(launch_sym_avg(Gb, bp, (int)bp, s));
-  // the iteration on [[C, Ḡ], [0, C]]/s: diagonal blocks (Y1, Z1, T1), off-diagonal (Y2, Z2, T2)
+  // the iteration on [[C, Ḡ], [0, C]]/s: diagonal blocks (Y1, Z1, T1) — the forward
+  // iterates, stored or recomputed — and off-diagonal blocks (Y2, Z2, T2)
   double *Y1 = M[0], *Z1 = M[1], *T1 = M[2], *Y1n = M[3], *Z1n = M[4], *Z2n = M[5],
          *Y2 = M[6], *Z2 = M[7], *T2 = M[8], *Y2n = M[9];
   HIPCHK(launch_ns_init(Gb, bp, (int)b, (int)bp, 1.0 / sc, 0.0, Y2, s));  // before Z2n reuses Gb
-  HIPCHK(launch_ns_init(PI, bp, (int)b, (int)bp, 1.0 / sc, 1.0, Y1, s));
-  HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 1.0, 1.0, Z1, s));
+  if (!stored) {
+    HIPCHK(launch_ns_init(PI, bp, (int)b, (int)bp, 1.0 / sc, 1.0, Y1, s));
+    HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 1.0, 1.0, Z1, s));
+  }
   HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 0.0, 0.0, Z2, s));
   for (int it = 0; it < used; ++it) {
-    if ((rc = sq(Z1, Y1, T1, -0.5, 0.0))) return rc;
-    HIPCHK(launch_diag_add_const(T1, bp, (int)bp, 1.5, s));
-    if ((rc = sq(Z1, Y2, T2, -0.5, 0.0))) return rc;
-    if ((rc = sq(Z2, Y1, T2, -0.5, 1.0))) return rc;
-    if ((rc = sq(Y1, T1, Y1n, 1.0, 0.0))) return rc;
-    if ((rc = sq(Y1, T2, Y2n, 1.0, 0.0))) return rc;
-    if ((rc = sq(Y2, T1, Y2n, 1.0, 1.0))) return rc;
-    if ((rc = sq(T1, Z1, Z1n, 1.0, 0.0))) return rc;
-    if ((rc = sq(T1, Z2, Z2n, 1.0, 0.0))) return rc;
-    if ((rc = sq(T2, Z1, Z2n, 1.0, 1.0))) return rc;
-    std::swap(Y1, Y1n);
+    const double *Yk = Y1, *Zkk = Z1, *Tk = T1;
+    if (stored) {
+      Yk = Ys[it];
+      Zkk = Zk[it];
+      Tk = Ts[it];
+    } else {
+      if ((rc = sym(Z1, Y1, T1, -0.5, 0.0))) return rc;
+      HIPCHK(launch_diag_add_const(T1, bp, (int)bp, 1.5, s));
+      HIPCHK(mirror(T1));
+    }
+    if ((rc = sym(Zkk, Y2, T2, -0.5, 0.0))) return rc;  // T2 = −½(Z1Y2 + Z2Y1)
+    if ((rc = sym(Z2, Yk, T2, -0.5, 1.0))) return rc;
+    HIPCHK(mirror(T2));
+    if ((rc = sym(Yk, T2, Y2n, 1.0, 0.0))) return rc;   // Y2 ← Y1T2 + Y2T1
+    if ((rc = sym(Y2, Tk, Y2n, 1.0, 1.0))) return rc;
+    HIPCHK(mirror(Y2n));
+    if ((rc = sym(Tk, Z2, Z2n, 1.0, 0.0))) return rc;   // Z2 ← T1Z2 + T2Z1
+    if ((rc = sym(T2, Zkk, Z2n, 1.0, 1.0))) return rc;
+    HIPCHK(mirror(Z2n));
+    if (!stored) {
+      if ((rc = sym(Y1, T1, Y1n, 1.0, 0.0))) return rc;
+      HIPCHK(mirror(Y1n));
+      if ((rc = sym(T1, Z1, Z1n, 1.0, 0.0))) return rc;
+      HIPCHK(mirror(Z1n));
+      std::swap(Y1, Y1n);
+      std::swap(Z1, Z1n);
+    }
     std::swap(Y2, Y2n);
-    std::swap(Z1, Z1n);
     std::swap(Z2, Z2n);
   }
+  T1 = M[2];
   // X = √s·Y2;  H = C X C (into T1);  G, g by fold_grad
   if ((rc = sq(Y2, PI, T2, rt, 0.0))) return rc;
   if ((rc = sq(PI, T2, T1, 1.0, 0.0))) return rc;

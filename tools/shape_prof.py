@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--grad", default=None, help="profile value_and_grad(objective) instead")
+    ap.add_argument("--block", default=None,
+                    help="profile block_loo(objective, grad=True) (dss / kc / es; ES: 300 draws)")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
     ctx = gpscore.Context(0)
@@ -44,6 +46,15 @@ def main():
     if args.grad:
         def unit():  # noqa: F811
             gp.value_and_grad(th, args.grad)
+    if args.block:
+        kw = {}
+        if args.block == "es":
+            import numpy as np
+            from gpscore.gp import es_draws
+            kw = {"num_sim": 300, "draws": es_draws(c["n"], 4, 300, np.random.default_rng(0))}
+
+        def unit():  # noqa: F811
+            gp.block_loo(th, args.block, grad=True, **kw)
     unit()
     ctx.synchronize()
     ctx.set_overlap(False)
