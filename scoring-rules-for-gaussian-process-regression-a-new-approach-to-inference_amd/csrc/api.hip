@@ -107,6 +107,7 @@ struct gps_ctx {
   // block-LOO scratch (per fold, reused): P, its L⁻¹ / P⁻¹ / H, vectors; full-GP Gblk, T;
   // FITC gradient: the fold's G_f, E_f, G_fE_f and F = Gblk E; energy score: work area, draws
   DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
+  DBuf ebuf_aux[3], bPIs, bRW;  // concurrent ES folds: work areas of the aux streams, C_f, r_f / w_f
   size_t bL_zeroed = 0;
   size_t lm_zeroed = 0, lb_zeroed = 0;
   int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
@@ -255,7 +256,8 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
   if (!st) st = ctx->stream;
   GemmParams q = p;
   if (q.map_mode == 0) q.map_mode = ctx->gemm_map;
-  if (epi == EPI_STORE && q.ksplit == 1 && !q.ws) {  // let gemm_plan split K on small grids
+  // the stream's slabs: gemm_plan may split K on small grids; an explicit 64-tile split uses them
+  if (epi == EPI_STORE && (q.ksplit == 1 || q.tile == 64) && !q.ws) {
     DBuf& ws = st == ctx->side      ? ctx->ws_side
                : st == ctx->look[0] ? ctx->ws_look[0]
                : st == ctx->look[1] ? ctx->ws_look[1]
@@ -568,10 +570,10 @@ int ns_iterations(double x0) {
 // (W = ∂ES/∂D ∘ D⁻¹); X with RX + XR = sym Ḡ is the off-diagonal block of the same iteration
 // run on [[C, Ḡ], [0, C]] (whose square root is [[R, X], [0, R]]); with w = C·∂ES/∂r:
 //   G = ∂ES/∂P_f = −CXC − ½(wrᵀ + rwᵀ),  g = ∂ES/∂α_f = w.
-int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int64_t bp,
-            const double* PI, const double* r, double trace_c, double* w, double* G, int64_t ldg,
-            double* g, double* out) {
-  hipStream_t s = ctx->stream;
+// Everything runs on stream s with work area eb (conc: one of 4 folds in flight).
+int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, const double* xi_src,
+            int64_t b, int64_t bp, const double* PI, const double* r, double trace_c, double* w,
+            double* G, int64_t ldg, double* g, double* out) {
   const int S = es.S;
   const int64_t Sp = pad_to(S + 1);
   const bool grad = G != nullptr;
@@ -586,8 +588,8 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
   const bool stored = nstore && nstore * bp * bp * 8 <= ((size_t)16 << 30);
   const size_t need = (size_t)(6 * Sp * bp + Sp * Sp + 2 * Sp + bp + 8) +
                       ((size_t)nmat + (stored ? nstore : 0)) * bp * bp;
-  HIPCHK(ensure(ctx->ebuf, need * 8));
-  double* q = ctx->ebuf.d();
+  HIPCHK(ensure(eb, need * 8));
+  double* q = eb.d();
   auto take = [&](int64_t cnt) {
     double* t = q;
     q += cnt;
@@ -611,7 +613,7 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
     GemmParams p = gp0();
     p.A = A; p.lda = lda; p.B = B; p.ldb = bp; p.C = C; p.ldc = bp;
     p.M = (int)rows; p.N = (int)bp; p.K = (int)kdim; p.alpha = alpha; p.beta = beta;
-    return gemm(ctx, al, LAY_N, EPI_STORE, p);
+    return gemm(ctx, al, LAY_N, EPI_STORE, p, s);
   };
   auto sq = [&](const double* A, const double* B, double* C, double alpha, double beta) {
     return mm(LAY_N, A, bp, B, C, bp, bp, alpha, beta);
@@ -624,7 +626,11 @@ int es_fold(gps_ctx* ctx, const EsArgs& es, const double* xi_src, int64_t b, int
     GemmParams p = gp0();
     p.A = A; p.lda = bp; p.B = B; p.ldb = bp; p.C = C; p.ldc = bp;
     p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.alpha = alpha; p.beta = beta; p.lower_out = 1;
-    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
+    if (conc) {  // 4 folds in flight: 2 K slices of 64-tiles (C2 ES: ks 1/2/3/4/auto(8) =
+      p.tile = 64;  // 54.8 / 53.9 / 54.4 / 55.3 / 58.5 ms per iteration)
+      p.ksplit = 2;
+    }
+    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, s);
   };
   auto mirror = [&](double* C) { return launch_sym_mirror(C, bp, (int)bp, s); };
   HIPCHK(launch_pad_copy(xi_src, b, xi, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
@@ -753,6 +759,17 @@ int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const doub
          *gm = v + 5 * bp, *gc = v + 6 * bp, *w = v + 7 * bp, *yf = v + 8 * bp;
   double* fs = v + 9 * bp;  // per fold: [Σ log L_ii, α·r, kc / es]
   const bool kc = objective == GPS_BLOCK_KC, esq = objective == GPS_BLOCK_ES;
+  // ES with the overlap option: the folds' square roots (hundreds of latency-bound b×b
+  // products each) run concurrently, fold f on stream f mod 4 with its own work area;
+  // C_f, r_f, w_f are kept per fold (the fold gradients land in disjoint blocks: full GP)
+  const bool es_conc = esq && ctx->overlap && nfold > 1;
+  double *PIs = nullptr, *RW = nullptr;
+  if (es_conc) {
+    HIPCHK(ensure(ctx->bPIs, (size_t)nfold * bp * bp * 8));
+    HIPCHK(ensure(ctx->bRW, (size_t)2 * nfold * bp * 8));
+    PIs = ctx->bPIs.d();
+    RW = ctx->bRW.d();
+  }
   int rc;
   // no reset_info here: a non-PD minor of the caller's main factor must still be reported
   HIPCHK(hipMemsetAsync(v, 0, (size_t)9 * bp * 8, s));
@@ -770,12 +787,18 @@ int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const doub
     if (kc)
       HIPCHK(launch_fold_terms(yf, r, c, (int)b, want_grad ? gm : nullptr, gc, fs + 3 * f + 2, s));
     if (!want_grad && !esq) continue;
+    double* PI = es_conc ? PIs + (int64_t)f * bp * bp : ctx->bPI.d();
     {  // C_f = P⁻¹ = Lp⁻ᵀLp⁻¹ (full)
       GemmParams p = gp0();
-      p.A = ctx->bL.d(); p.lda = bp; p.B = ctx->bL.d(); p.ldb = bp; p.C = ctx->bPI.d(); p.ldc = bp;
+      p.A = ctx->bL.d(); p.lda = bp; p.B = ctx->bL.d(); p.ldb = bp; p.C = PI; p.ldc = bp;
       p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.tri = TRI_K_GE_I; p.lower_out = 1;
       if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
-      HIPCHK(launch_sym_mirror(ctx->bPI.d(), bp, (int)bp, s));
+      HIPCHK(launch_sym_mirror(PI, bp, (int)bp, s));
+    }
+    if (es_conc) {  // r_f for the concurrent pass below
+      HIPCHK(hipMemcpyAsync(RW + (int64_t)2 * f * bp, r, (size_t)bp * 8, hipMemcpyDeviceToDevice,
+                            s));
+      continue;
     }
     double* G = nullptr;
     int64_t ldg = 0;
@@ -785,7 +808,7 @@ int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const doub
       ldg = dst.second;
     }
     if (esq) {
-      if ((rc = es_fold(ctx, *es, es->draws + 2 * (int64_t)es->S * a, b, bp, ctx->bPI.d(), r, 0.0,
+      if ((rc = es_fold(ctx, s, ctx->ebuf, false, *es, es->draws + 2 * (int64_t)es->S * a, b, bp, ctx->bPI.d(), r, 0.0,
                         w, G, ldg, want_grad ? g + a : nullptr, fs + 3 * f + 2)))
         return rc;
     } else if (!kc) {  // DSS: G_f = −½(P⁻¹ + r rᵀ), g_f = r
@@ -801,6 +824,39 @@ int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const doub
                               -1.0, 0.0, -1.0, G, ldg, g + a, s));
     }
     if (want_grad && (rc = gdone(f, a, b))) return rc;
+  }
+  if (es_conc) {
+    hipStream_t st[4] = {s, ctx->side, ctx->look[0], ctx->look[1]};
+    DBuf* eb[4] = {&ctx->ebuf, &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2]};
+    const int nst = std::min(nfold, 4);
+    hipEvent_t fork = sync_event(ctx);
+    if (!fork) return fail(ctx, -2, "hipEventCreate failed");
+    HIPCHK(hipEventRecord(fork, s));
+    for (int k = 1; k < nst; ++k) HIPCHK(hipStreamWaitEvent(st[k], fork, 0));
+    for (int f = 0; f < nfold; ++f) {
+      const int64_t a = bnd[f], b = bnd[f + 1] - bnd[f];
+      double* G = nullptr;
+      int64_t ldg = 0;
+      if (want_grad) {
+        const std::pair<double*, int64_t> dst = gdst(a, b);
+        G = dst.first;
+        ldg = dst.second;
+      }
+      double* rf = RW + (int64_t)2 * f * bp;
+      if ((rc = es_fold(ctx, st[f % 4], *eb[f % 4], true, *es, es->draws + 2 * (int64_t)es->S * a, b,
+                        bp, PIs + (int64_t)f * bp * bp, rf, 0.0, rf + bp, G, ldg,
+                        want_grad ? g + a : nullptr, fs + 3 * f + 2)))
+        return rc;
+    }
+    for (int k = 1; k < nst; ++k) {
+      hipEvent_t join = sync_event(ctx);
+      if (!join) return fail(ctx, -2, "hipEventCreate failed");
+      HIPCHK(hipEventRecord(join, st[k]));
+      HIPCHK(hipStreamWaitEvent(s, join, 0));
+    }
+    if (want_grad)
+      for (int f = 0; f < nfold; ++f)
+        if ((rc = gdone(f, bnd[f], bnd[f + 1] - bnd[f]))) return rc;
   }
   std::vector<double> h((size_t)3 * nfold);
   HIPCHK(hipMemcpyAsync(h.data(), fs, h.size() * 8, hipMemcpyDeviceToHost, s));
@@ -886,7 +942,8 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
-                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws, &ctx->ws_syrk};
+                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws, &ctx->ws_syrk,
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
@@ -1963,7 +2020,7 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
   es.beta = beta;
   es.draws = ctx->edraws.d();
   double* dev_out = ctx->small.d();
-  if (int rc = es_fold(ctx, es, es.draws, b, bp, ctx->bPI.d(), ctx->t1.d(), tr, ctx->t2.d(),
+  if (int rc = es_fold(ctx, s, ctx->ebuf, false, es, es.draws, b, bp, ctx->bPI.d(), ctx->t1.d(), tr, ctx->t2.d(),
                        nullptr, 0, nullptr, dev_out))
     return rc;
   HIPCHK(hipMemcpyAsync(ctx->hsmall, dev_out, 8, hipMemcpyDeviceToHost, s));

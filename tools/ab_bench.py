@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--block", default=None,
+                    help="time block_loo(objective, grad=True) (dss / kc / es; ES: 300 draws)")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
@@ -45,6 +47,14 @@ def main():
     def unit():
         gp.fit(theta=th, return_loo=False)
         gp.predict(with_scores=True)
+    if args.block:
+        kw = {}
+        if args.block == "es":
+            from gpscore.gp import es_draws
+            kw = {"num_sim": 300, "draws": es_draws(c["n"], 4, 300, np.random.default_rng(0))}
+
+        def unit():  # noqa: F811
+            gp.block_loo(th, args.block, grad=True, **kw)
 
     variants = []
     for v in args.variants:
