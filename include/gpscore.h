@@ -86,6 +86,9 @@ enum {
                              resident workgroups; 0 (default, measured faster end-to-end on
                              C3 because the overlap streams already fill it): one launch.  Same numerics up to
                              the order of the K summation (deterministic either way). */
+  GPS_OPT_GRAM_REG = 9,    /* 1 (default): Gram builds with d in {1, 8, 16} keep the column
+                             features in registers (128×128 tiles); 0: the LDS-column kernel.
+                             Bitwise-identical output.  Process-wide. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -982,6 +982,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
     case GPS_OPT_FUSED_SPLITK: ctx->fused_splitk = value != 0; return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
+    case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_SYRK_SPLIT: ctx->syrk_split = value != 0; return 0;
     case GPS_OPT_MAIN_CU_EXCLUDE: {  // recreate the (owned) main stream CU-masked
       ARGCHK(ctx->own_stream, "the main stream is caller-owned");

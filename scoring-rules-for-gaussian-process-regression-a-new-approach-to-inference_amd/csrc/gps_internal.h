@@ -75,6 +75,7 @@ struct GemmParams {
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
 struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
+extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
 extern int g_tiny_gemm;  // 1: M·N <= 256², K <= 1024 GEMMs use the one-wave-per-16² kernel
 
 // ------------------------------------------------------------ device reductions

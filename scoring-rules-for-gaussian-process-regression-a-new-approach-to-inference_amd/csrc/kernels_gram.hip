@@ -89,9 +89,98 @@ __global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
   }
 }
 
+// Register-resident variant for the compiled feature counts (d = 1, 8, 16): a 128×128
+// tile per workgroup, each lane holds its two columns' scaled features in VGPRs for the
+// whole tile and the 128 rows' scaled features sit in LDS, read as wave-uniform
+// (broadcast) 16-byte loads.  Per element that is 2d VALU ops + exp and no per-element
+// LDS traffic — gram_kernel above spends one ds_read_b128 per lane per feature per row
+// on the columns, which made it LDS-issue-bound at d = 16 (C5 Knm: 2.0 TB/s).  Same
+// arithmetic in the same order as gram_kernel: bitwise-identical output.
+constexpr int G2_ROWS = 128;
+
+template <int D>
+__global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
+  __shared__ __attribute__((aligned(16))) double xs_row[G2_ROWS * D];
+  const int tiles_x = p.N / GR_COLS;
+  const int bx = blockIdx.x % tiles_x;
+  const int by = blockIdx.x / tiles_x;
+  const int c0 = bx * GR_COLS, r0 = by * G2_ROWS;
+  if (p.lower && c0 > r0 + G2_ROWS - 1) return;
+  const int rows = min(G2_ROWS, p.M - r0);
+  const int tid = threadIdx.x;
+  for (int e = tid; e < rows * D; e += 256) {
+    const int i = e / D, k = e - i * D;
+    const int gi = r0 + i;
+    xs_row[e] = gi < p.n ? p.x[(int64_t)gi * D + k] * p.inv_ell[k] : 0.0;
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  const int gj = c0 + 2 * lane;
+  const bool colpad0 = gj >= p.m, colpad1 = gj + 1 >= p.m;
+  double f0[D], f1[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    f0[k] = colpad0 ? 0.0 : p.xp[(int64_t)gj * D + k] * p.inv_ell[k];
+    f1[k] = colpad1 ? 0.0 : p.xp[(int64_t)(gj + 1) * D + k] * p.inv_ell[k];
+  }
+  __syncthreads();
+
+#pragma unroll 2
+  for (int rr = wave; rr < rows; rr += 4) {
+    const int gi = r0 + rr;
+    double a0 = 0.0, a1 = 0.0;
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+      for (int k = 0; k < D; k += 2) {
+        const double2 xr = *reinterpret_cast<const double2*>(&xs_row[rr * D + k]);
+        double e0 = xr.x - f0[k], e1 = xr.x - f1[k];
+        a0 = fma(e0, e0, a0);
+        a1 = fma(e1, e1, a1);
+        e0 = xr.y - f0[k + 1];
+        e1 = xr.y - f1[k + 1];
+        a0 = fma(e0, e0, a0);
+        a1 = fma(e1, e1, a1);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double xr = xs_row[rr * D + k];
+        const double e0 = xr - f0[k], e1 = xr - f1[k];
+        a0 = fma(e0, e0, a0);
+        a1 = fma(e1, e1, a1);
+      }
+    }
+    double v0 = p.sf2 * exp(-0.5 * a0);
+    double v1 = p.sf2 * exp(-0.5 * a1);
+    const bool rowpad = gi >= p.n;
+    if (gi == gj) v0 += p.diag_add;
+    if (gi == gj + 1) v1 += p.diag_add;
+    if (rowpad || colpad0) v0 = (p.pad_identity && gi == gj) ? 1.0 : 0.0;
+    if (rowpad || colpad1) v1 = (p.pad_identity && gi == gj + 1) ? 1.0 : 0.0;
+    double* dst = p.out + (int64_t)gi * p.ldo + gj;
+    if (!p.lower || gj + 1 <= gi) {
+      *reinterpret_cast<double2*>(dst) = make_double2(v0, v1);
+    } else if (gj <= gi) {
+      dst[0] = v0;
+    }
+  }
+}
+
+int g_gram_reg = 1;  // GPS_OPT_GRAM_REG (process-wide; 0 = the LDS-column kernel for every d)
+
 hipError_t launch_gram(const GramParams& p, hipStream_t s) {
   if (p.d < 1 || p.d > GPS_MAX_D || p.M % GR_ROWS || p.N % GR_COLS || (p.ldo & 1))
     return hipErrorInvalidValue;
+  if (g_gram_reg && (p.d == 1 || p.d == 8 || p.d == 16)) {
+    const int64_t blocks = (int64_t)((p.M + G2_ROWS - 1) / G2_ROWS) * (p.N / GR_COLS);
+    if (blocks == 0) return hipSuccess;
+    dim3 grid((unsigned)blocks), block(256);
+    switch (p.d) {
+      case 1: hipLaunchKernelGGL(gram_reg_kernel<1>, grid, block, 0, s, p); break;
+      case 8: hipLaunchKernelGGL(gram_reg_kernel<8>, grid, block, 0, s, p); break;
+      default: hipLaunchKernelGGL(gram_reg_kernel<16>, grid, block, 0, s, p); break;
+    }
+    return hipGetLastError();
+  }
   const int64_t blocks = (int64_t)(p.M / GR_ROWS) * (p.N / GR_COLS);
   if (blocks == 0) return hipSuccess;
   dim3 grid((unsigned)blocks), block(256);

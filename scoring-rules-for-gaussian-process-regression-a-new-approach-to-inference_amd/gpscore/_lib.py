@@ -19,6 +19,7 @@ GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_LOOKAHEAD, GPS_OPT_RESERVE_CUS, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN = 0, 1, 2, 3, 4
 GPS_OPT_FUSED_SPLITK, GPS_OPT_MAIN_CU_EXCLUDE, GPS_OPT_TINY_GEMM, GPS_OPT_SYRK_SPLIT = 5, 6, 7, 8
+GPS_OPT_GRAM_REG = 9
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
@@ -180,6 +181,11 @@ class Context:
         """One-wave-per-16×16 kernel for the small GEMMs at the bottom of the recursion
         (default) or the 64-tile split-K path (process-wide)."""
         self.call("gps_ctx_set_option", GPS_OPT_TINY_GEMM, 1 if on else 0)
+
+    def set_gram_reg(self, on=True):
+        """Register-resident Gram kernel for d in {1, 8, 16} (default) or the LDS-column
+        kernel; bitwise-identical output (process-wide)."""
+        self.call("gps_ctx_set_option", GPS_OPT_GRAM_REG, 1 if on else 0)
 
     def set_syrk_split(self, on=True):
         """Fill-model split-K for the factorisation's big trailing updates, or one launch

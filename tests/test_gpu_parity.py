@@ -164,6 +164,34 @@ def test_not_positive_definite_raises(gp):
 
 
 # ------------------------------------------------------------------- L1 blocks
+@pytest.mark.parametrize("d", [1, 8, 16])
+@pytest.mark.parametrize("uplo", [0, 1])
+def test_gram_reg_kernel_bitwise(gpu_ctx, d, uplo):
+    """The register-resident Gram kernel (d in {1, 8, 16}) against the LDS-column kernel:
+    same arithmetic in the same order, so bitwise-identical output, including the padded
+    rows/columns (n, m not multiples of 128), the lower mask and the diagonal add."""
+    from gpscore._lib import GPS_ARD, ptr
+    rng = np.random.default_rng(10 + d)
+    n, m = 333, 333 if uplo else 201
+    x = rng.standard_normal((n, d))
+    xp = x if uplo else rng.standard_normal((m, d))
+    ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
+    outs = []
+    for on in (False, True):
+        gpu_ctx.set_gram_reg(on)
+        out = np.full((n, m), -7.0)
+        gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), n, ptr(xp), m, d, 0.3, ptr(ell), d, 0.01,
+                     uplo, ptr(out))
+        outs.append(out)
+    gpu_ctx.set_gram_reg(True)
+    assert np.array_equal(outs[0], outs[1])
+    ref = O.fast_gram(x, xp, 0.3, ell) + 0.01 * np.eye(n, m)  # diag_add goes on i == j
+    mask = np.tril(np.ones((n, m), bool)) if uplo else np.ones((n, m), bool)
+    assert nrel(outs[1][mask], ref[mask]) < 1e-13
+    if uplo:
+        assert np.all(outs[1][~mask] == 0.0)  # gps_gram zero-fills the unwritten half
+
+
 def test_gram_kernel(gpu_ctx):
     from gpscore import compat
     g = load_golden("l1_blocks")

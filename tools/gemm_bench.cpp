@@ -136,6 +136,33 @@ static int syrk_study(double* A, double* B, double* C) {
   return 0;
 }
 
+// layout study: the 10k-level triangular products of the C3 recursion in all four operand
+// layouts (does storing T transposed / keeping L⁻ᵀ turn the NN products into faster ones?)
+static int layout_study(double* A, double* B, double* C) {
+  struct S { const char* name; int M, N, K, tri; } cs[] = {
+    {"K_LE_I 10112x9984x10112", 10112, 9984, 10112, TRI_K_LE_I},
+    {"K_GE_J 10112x9984x9984", 10112, 9984, 9984, TRI_K_GE_J},
+    {"K_LE_J 10112x9984x9984", 10112, 9984, 9984, TRI_K_LE_J},
+    {"K_LE_I 5120x4992x5120", 5120, 4992, 5120, TRI_K_LE_I},
+    {"K_GE_J 5120x4992x4992", 5120, 4992, 4992, TRI_K_GE_J},
+    {"NONE 8192^3", 8192, 8192, 8192, TRI_NONE},
+  };
+  const char* nm[2] = {"N", "T"};
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (auto& c : cs)
+    for (int al = 0; al < 2; ++al)
+      for (int bl = 0; bl < 2; ++bl) {
+        p.A = A; p.B = B; p.C = C; p.alpha = 1.0; p.beta = 0.0; p.ksplit = 1; p.tile = 0;
+        p.lda = al == LAY_N ? c.K : c.M;
+        p.ldb = bl == LAY_T ? c.K : c.N;
+        p.ldc = c.N;
+        p.M = c.M; p.N = c.N; p.K = c.K; p.tri = c.tri; p.lower_out = 0; p.map_mode = 0;
+        const double fl = (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.K;
+        printf("%-26s %s%s %7.2f TF/s\n", c.name, nm[al], nm[bl], run(al, bl, EPI_STORE, p, 5, fl));
+      }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 20480;
   double *A, *B, *C, *o0, *o1, *w;
@@ -151,6 +178,7 @@ int main(int argc, char** argv) {
   printf("operands: %s\n", zeros ? "zeros" : "uniform random [-0.5, 0.5)");
   if (argc > 1 && !strcmp(argv[1], "ld")) return ldstudy(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "syrk")) return syrk_study(A, B, C);
+  if (argc > 1 && !strcmp(argv[1], "layout")) return layout_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "sweep")) {
     double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);
     return sweep(A, B, C, ws);
