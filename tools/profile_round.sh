@@ -10,8 +10,9 @@ export TMPDIR=/tmp
 BENCH="bench.py --steps 2 --warmup 1 --no-cpu"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run \
   -- python3 $BENCH > $OUT/trace.log 2>&1
-# counters on a shorter run (every dispatch is serialised and sampled)
-PBENCH="bench.py --steps 1 --warmup 0 --no-cpu --no-fitc"
+# counters on a shorter run of the headline unit only (every dispatch is serialised and
+# sampled), so the per-launch averages match the launches the roofline objects time
+PBENCH="bench.py --steps 1 --warmup 0 --no-cpu --no-fitc --no-grad --no-block"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run \
   -- python3 $PBENCH > $OUT/fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run \

@@ -54,13 +54,13 @@ def main(d):
                       "instantiations": lst}
     # per-launch averages the bench's roofline objects quote (full-GP-only counter run:
     # the bench step runs its timed passes once each in the counter run)
-    def avg(prefix):
-        ks = [k for k in summary if k.startswith(prefix)]
+    def avg(*prefixes):
+        ks = [k for k in summary if k.startswith(prefixes)]
         n = sum(summary[k]["launches"] for k in ks)
         b = sum(summary[k]["hbm_bytes_per_launch"] * summary[k]["launches"] for k in ks)
         return b / n if n else None
     summary["_roofline"] = {"gemm_per_launch_bytes": avg("gps::gemm_f64_kernel"),
-                            "gram_per_launch_bytes": avg("gps::gram_kernel"),
+                            "gram_per_launch_bytes": avg("gps::gram_kernel", "gps::gram_reg_kernel"),
                             "note": "HBM bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 "
                                     "FETCH_SIZE half-count correction), per launch"}
     json.dump(summary, open(os.path.join(d, "traffic.json"), "w"), indent=1)
