@@ -8,7 +8,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-for p in (PKG_DIR, os.path.join(ROOT, "oracle")):
+for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
