@@ -145,6 +145,7 @@ hipError_t launch_fitc_grad_mdiag(const double* KN, int64_t ldkn, const double* 
 //   acc: Σ GK, Σ GK Δ_k² (this pass's dims), and per column Σ_i GK Δ_k (→ Z gradient)
 constexpr int FG_COLS = 64;
 constexpr int FG_DP = 16;
+constexpr int FG_U = 4;  // rows per thread per batch (loads issued together)
 
 template <int D>
 __global__ __launch_bounds__(256) void fitc_grad_contract_kernel(FitcContractParams p) {
@@ -177,40 +178,66 @@ __global__ __launch_bounds__(256) void fitc_grad_contract_kernel(FitcContractPar
     double qj[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) qj[q] = p.pc[q] != 0.0 ? p.qv[q][j] : 0.0;
-    for (int i = r0 + rg; i < r1; i += 4) {
-      const int iu = __builtin_amdgcn_readfirstlane(i);  // wave-uniform row
-      const double* xri = p.xr + (int64_t)iu * d;
-      double r2 = 0.0;
-      if constexpr (D > 0) {
+    // rows in batches of FG_U per thread: every R[t] load (and the wave-uniform rs[t][i]
+    // scalar loads) of the batch is issued before the first element's arithmetic, so
+    // FG_U·nt HBM reads are in flight per wave instead of one (the one-row loop waited
+    // out a full HBM latency per element).  Rows are still accumulated in ascending order,
+    // so the sums are bitwise those of the one-row loop.
+    for (int i0 = r0 + rg; i0 < r1; i0 += 4 * FG_U) {
+      double Rv[FG_U][4], rsv[FG_U][4];
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          const double t = xri[k] * p.inv_ell[k] - xj[k];
-          r2 = fma(t, t, r2);
-        }
-      } else {
-        for (int k = 0; k < d; ++k) {
-          const double t = xri[k] * p.inv_ell[k] - xs[cj * d + k];
-          r2 = fma(t, t, r2);
+      for (int u = 0; u < FG_U; ++u) {
+        const int iu = __builtin_amdgcn_readfirstlane(i0 + 4 * u);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          Rv[u][t] = 0.0;
+          rsv[u][t] = 1.0;
+          if (iu < r1 && t < p.nt) {
+            Rv[u][t] = p.R[t][(int64_t)iu * p.ldr[t] + j];
+            if (p.rs[t]) rsv[u][t] = p.rs[t][iu];
+          }
         }
       }
-      const double Kij = p.sf2 * exp(-0.5 * r2);
-      double G = 0.0;
-      for (int t = 0; t < p.nt; ++t) {
-        const double sc = p.rs[t] ? p.coef[t] * p.rs[t][iu] : p.coef[t];
-        G = fma(sc, p.R[t][(int64_t)iu * p.ldr[t] + j], G);
-      }
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (p.pc[q] != 0.0) G = fma(p.pc[q] * p.pv[q][iu], qj[q], G);
-      const double gk = G * Kij;
-      acc[0] += gk;
+      for (int u = 0; u < FG_U; ++u) {
+        const int iu = __builtin_amdgcn_readfirstlane(i0 + 4 * u);
+        if (iu >= r1) break;
+        const double* xri = p.xr + (int64_t)iu * d;
+        double r2 = 0.0;
+        if constexpr (D > 0) {
 #pragma unroll
-      for (int q = 0; q < FG_DP; ++q) {
-        if (D > 0 ? q < D : d0 + q < d) {
-          const double t = D > 0 ? xri[q] * p.inv_ell[q] - xj[q]
-                                 : xri[d0 + q] * p.inv_ell[d0 + q] - xs[cj * d + d0 + q];
-          acc[1 + q] = fma(gk, t * t, acc[1 + q]);
-          zacc[q] = fma(gk, t, zacc[q]);
+          for (int k = 0; k < D; ++k) {
+            const double tk = xri[k] * p.inv_ell[k] - xj[k];
+            r2 = fma(tk, tk, r2);
+          }
+        } else {
+          for (int k = 0; k < d; ++k) {
+            const double tk = xri[k] * p.inv_ell[k] - xs[cj * d + k];
+            r2 = fma(tk, tk, r2);
+          }
+        }
+        const double Kij = p.sf2 * exp(-0.5 * r2);
+        double G = 0.0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < p.nt) {
+            const double sc = p.rs[t] ? p.coef[t] * rsv[u][t] : p.coef[t];
+            G = fma(sc, Rv[u][t], G);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (p.pc[q] != 0.0) G = fma(p.pc[q] * p.pv[q][iu], qj[q], G);
+        const double gk = G * Kij;
+        acc[0] += gk;
+#pragma unroll
+        for (int q = 0; q < FG_DP; ++q) {
+          if (D > 0 ? q < D : d0 + q < d) {
+            const double tq = D > 0 ? xri[q] * p.inv_ell[q] - xj[q]
+                                    : xri[d0 + q] * p.inv_ell[d0 + q] - xs[cj * d + d0 + q];
+            acc[1 + q] = fma(gk, tq * tq, acc[1 + q]);
+            zacc[q] = fma(gk, tq, zacc[q]);
+          }
         }
       }
     }
