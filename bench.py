@@ -320,6 +320,7 @@ def main():
         fitc = {}
         legs = ["C5"] + (["C4"] if world == 1 else [])
         fgp = gpscore.GP(ctx=ctx)
+        comm_err = None
         if world > 1 and not args.rehearse:
             import ctypes
             lib = gpscore.load()
@@ -330,7 +331,15 @@ def main():
                 uid = buf.raw
             obj_l = [uid]
             ctl.dist.broadcast_object_list(obj_l, src=0)
-            ctx.call("gps_comm_init", world, rank, ctypes.create_string_buffer(obj_l[0], 128))
+            try:
+                ctx.call("gps_comm_init", world, rank, ctypes.create_string_buffer(obj_l[0], 128))
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line, not fatal
+                comm_err = repr(e)
+            # every rank learns whether any communicator failed (over gloo, so no rank is
+            # left waiting in an RCCL collective); the headline is already measured
+            if ctl.max(1.0 if comm_err else 0.0) > 0:
+                legs = []
+                fitc["error"] = comm_err or "gps_comm_init failed on another rank"
         for leg in legs:
             fc = CONFIGS[leg]
             Xf, yf, Xtf, ytf, Z, thf = synth(fc["n"], fc["d"], fc["nt"], fc["seed"], fc["m"])
@@ -374,7 +383,7 @@ def main():
                                       "note": "4 folds of 10 000 rows, theta and Z gradient"}
                 fitc[leg]["grad"] = fg
             del Xf, yf, Xtf, ytf
-        if world > 1 and not args.rehearse:
+        if world > 1 and not args.rehearse and "error" not in fitc:
             ctx.call("gps_comm_destroy")
         res["fitc"] = fitc
 
