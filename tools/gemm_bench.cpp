@@ -163,6 +163,24 @@ static int layout_study(double* A, double* B, double* C) {
   return 0;
 }
 
+// FITC row-norm products ‖L⁻¹k_i‖² (EPI_ROWSQ, K ≤ j triangular) at the C4 / C5 shapes under
+// every tile order: tall-skinny grids where each A row panel feeds all N/128 column tiles
+static int rowsq_study(double* A, double* B, double* o0) {
+  struct S { const char* name; int M, N; } cs[] = {
+    {"C4 fit  40064x2048", 40064, 2048}, {"C4 pred 10112x2048", 10112, 2048},
+    {"C5/2    100032x4096", 100032, 4096}};
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (auto& c : cs)
+    for (int mm = 0; mm < 4; ++mm) {
+      p.A = A; p.B = B; p.out0 = o0; p.alpha = 1.0; p.ksplit = 1; p.tile = 0;
+      p.lda = c.N; p.ldb = c.N; p.ld_out = c.M;
+      p.M = c.M; p.N = c.N; p.K = c.N; p.tri = TRI_K_LE_J; p.map_mode = mm;
+      const double fl = (double)c.M * c.N * c.N;
+      printf("rowsq %-22s map%d %7.2f TF/s\n", c.name, mm, run(LAY_N, LAY_T, EPI_ROWSQ, p, 5, fl));
+    }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 20480;
   double *A, *B, *C, *o0, *o1, *w;
@@ -179,6 +197,7 @@ int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "ld")) return ldstudy(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "syrk")) return syrk_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "layout")) return layout_study(A, B, C);
+  if (argc > 1 && !strcmp(argv[1], "rowsq")) return rowsq_study(A, B, o0);
   if (argc > 1 && !strcmp(argv[1], "sweep")) {
     double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);
     return sweep(A, B, C, ws);
