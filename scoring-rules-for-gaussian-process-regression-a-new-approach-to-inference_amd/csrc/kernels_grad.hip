@@ -98,6 +98,7 @@ hipError_t launch_sym_mirror(double* M, int64_t ld, int n_pad, hipStream_t s) {
 // Dimensions beyond DP per pass take extra passes (blockIdx.y), each re-reading M.
 constexpr int GT = 64;
 constexpr int DP = 16;
+constexpr int GU = 4;  // rows per thread per load batch
 
 // D > 0: compile-time feature count (the column's scaled features live in registers);
 // D = 0: runtime d <= GPS_MAX_D (features from LDS).  Row features are read from LDS by
@@ -133,44 +134,59 @@ __global__ __launch_bounds__(256) void grad_contract_kernel(GradParams p) {
   for (int q = 0; q < 2 + DP; ++q) acc[q] = 0.0;
   if (j < p.n) {
     const double aj = p.alpha[j], vj = p.v ? p.v[j] : 0.0;
-    for (int rr = rg; rr < GT; rr += 4) {
-      const int i = row0 + rr;
-      if (i >= p.n || i < j) continue;
-      double r2 = 0.0;
-      if constexpr (D > 0) {
+    // rows in batches of GU per thread: the batch's M loads (Ainv, Mx) are all issued before
+    // the first element's arithmetic instead of one HBM latency per element; rows are still
+    // accumulated in ascending order (bitwise the one-row loop's sums)
+    for (int rb = rg; rb < GT; rb += 4 * GU) {
+      double ldA[GU], ldX[GU];
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          const double t = xr[rr * D + k] - xj[k];
-          r2 = fma(t, t, r2);
-        }
-      } else {
-        for (int k = 0; k < d; ++k) {
-          const double t = xr[rr * d + k] - xc[cj * d + k];
-          r2 = fma(t, t, r2);
-        }
+      for (int u = 0; u < GU; ++u) {
+        const int i = row0 + rb + 4 * u;
+        const bool ok = i < p.n && i >= j;
+        ldA[u] = ok && p.a0 != 0.0 ? p.Ainv[(int64_t)i * p.ldm + j] : 0.0;
+        ldX[u] = ok && p.a3 != 0.0 ? p.Mx[(int64_t)i * p.ldm + j] : 0.0;
       }
-      const double K = p.sf2 * exp(-0.5 * r2);
-      const double ai = p.alpha[i];
-      double m = p.a1 * ai * aj;
-      if (p.a0 != 0.0) m = fma(p.a0, p.Ainv[(int64_t)i * p.ldm + j], m);
-      if (p.a2 != 0.0) m = fma(p.a2, 0.5 * (p.v[i] * aj + ai * vj), m);
-      if (p.a3 != 0.0) m = fma(p.a3, p.Mx[(int64_t)i * p.ldm + j], m);
-      const double w = i == j ? 1.0 : 2.0;
-      const double mk = w * m * K;
-      acc[0] += mk;
-      if (i == j) acc[1] += m;
-      if constexpr (D > 0) {  // D <= DP: one pass, d0 == 0
 #pragma unroll
-        for (int q = 0; q < D; ++q) {
-          const double t = xr[rr * D + q] - xj[q];
-          acc[2 + q] = fma(mk, t * t, acc[2 + q]);
+      for (int u = 0; u < GU; ++u) {
+        const int rr = rb + 4 * u;
+        const int i = row0 + rr;
+        if (i >= p.n || i < j) continue;
+        double r2 = 0.0;
+        if constexpr (D > 0) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            const double t = xr[rr * D + k] - xj[k];
+            r2 = fma(t, t, r2);
+          }
+        } else {
+          for (int k = 0; k < d; ++k) {
+            const double t = xr[rr * d + k] - xc[cj * d + k];
+            r2 = fma(t, t, r2);
+          }
         }
-      } else {
+        const double K = p.sf2 * exp(-0.5 * r2);
+        const double ai = p.alpha[i];
+        double m = p.a1 * ai * aj;
+        if (p.a0 != 0.0) m = fma(p.a0, ldA[u], m);
+        if (p.a2 != 0.0) m = fma(p.a2, 0.5 * (p.v[i] * aj + ai * vj), m);
+        if (p.a3 != 0.0) m = fma(p.a3, ldX[u], m);
+        const double w = i == j ? 1.0 : 2.0;
+        const double mk = w * m * K;
+        acc[0] += mk;
+        if (i == j) acc[1] += m;
+        if constexpr (D > 0) {  // D <= DP: one pass, d0 == 0
 #pragma unroll
-        for (int q = 0; q < DP; ++q) {
-          if (d0 + q < d) {
-            const double t = xr[rr * d + d0 + q] - xc[cj * d + d0 + q];
+          for (int q = 0; q < D; ++q) {
+            const double t = xr[rr * D + q] - xj[q];
             acc[2 + q] = fma(mk, t * t, acc[2 + q]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < DP; ++q) {
+            if (d0 + q < d) {
+              const double t = xr[rr * d + d0 + q] - xc[cj * d + d0 + q];
+              acc[2 + q] = fma(mk, t * t, acc[2 + q]);
+            }
           }
         }
       }
