@@ -61,6 +61,8 @@ def _gram(kind, x, xp, a, b):
     x, xp = f64(_np(x), 2), f64(_np(xp), 2)
     ell = np.ascontiguousarray(_np(b).ravel())
     out = np.empty((x.shape[0], xp.shape[0]))
+    if out.size == 0:  # torch returns the empty n×m product for an empty side (KF:15-21)
+        return out
     _ctx().call("gps_gram", kind, ptr(x), x.shape[0], ptr(xp), xp.shape[0], x.shape[1],
                 _scalar(a), ptr(ell), ell.size, 0.0, GPS_FULL, ptr(out))
     return out
@@ -177,6 +179,8 @@ def _scores(m, c, y, yp=None):
     else:
         ypv = f64(_np(yp)).ravel()
         mu0, v0 = float(ypv.mean()), float(ypv.var(ddof=1))
+    if y.size == 0:  # torch.mean over no points is NaN (KF:57, KF:68), not an error
+        return np.full(6, np.nan)
     out = np.zeros(6)
     _ctx().call("gps_scores", ptr(m), ptr(c), ptr(y), y.size, mu0, v0, ptr(out))
     return out

@@ -114,3 +114,18 @@ def test_fitc_gloo_world2(tmp_path, name):
         assert abs(float(r["var"]) - g["y"].var(ddof=1)) < 1e-12
         for k in ("nlml", "loo_crps", "loo_logs"):
             assert abs(float(r[k]) - float(g[k])) <= 1e-8 * max(1, abs(float(g[k]))), k
+
+
+def test_compat_empty_inputs_follow_torch():
+    """Empty sides: the reference's ARD is an n×m product (KF:15-21), so an empty side gives
+    an empty matrix; crps / logs / MSLL / SMSE are means over the points (KF:52-68, 110-134),
+    which torch evaluates to NaN over no points.  Neither reaches the device."""
+    from gpscore import compat
+    x = np.zeros((0, 3))
+    xp = np.ones((4, 3))
+    assert compat.ARD(x, xp, 0.0, np.zeros(3)).shape == (0, 4)
+    assert compat.rbf(xp, x, 0.0, 0.0).shape == (4, 0)
+    e = np.zeros(0)
+    assert np.isnan(compat.crps(e, e, e)) and np.isnan(compat.logs(e, e, e))
+    assert np.isnan(compat.trivial_loss(e, e, e, np.ones(3)))
+    assert np.isnan(compat.SMSE(e, e, np.ones(3)))
