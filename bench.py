@@ -161,6 +161,20 @@ def roofline_mfma(prof, traffic=None, steps=1):
             "flop_per_launch": f / n if n else None}
 
 
+def roofline_trailing(prof, steps=1):
+    """The Cholesky trailing updates A22 -= L21 L21ᵀ alone (the lower-tile SYRK launches of
+    the recursion, every size class) — the MFMA-utilisation figure north_star names."""
+    ks = [k for k in prof if k.startswith("gemm_syrk")]
+    f = sum(prof[k]["flop"] for k in ks) / steps
+    ms = sum(prof[k]["ms"] for k in ks) / steps
+    n = sum(prof[k]["count"] for k in ks) / steps
+    ach = f / (ms * 1e-3) / 1e12 if ms else 0.0
+    return {"bound": "mfma", "kernel": "gemm_f64_kernel lower-tile SYRK (trailing updates)",
+            "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_FP64_TFLOPS, 4), "launches_per_step": n,
+            "ms_per_step": ms, "flop_per_step": f}
+
+
 def roofline_gram(prof, steps=1, traffic=None, tags=("gram_kff", "gram_ksf")):
     b = sum(prof[t]["bytes"] for t in tags if t in prof) / steps
     ms = sum(prof[t]["ms"] for t in tags if t in prof) / steps
@@ -270,6 +284,7 @@ def main():
                    "parallelism": "replicas" if world > 1 else "single"},
         "roofline": roofline_mfma(prof, traffic, args.steps),
         "roofline_gram": roofline_gram(prof, args.steps, traffic_gram),
+        "roofline_trailing_update": roofline_trailing(prof, args.steps),
         "objectives": obj, "scores": sc,
         "kernels_per_step": kernel_summary(prof, args.steps),
         "kernel_accounting": {"ms_per_step": ms_acct, "streams": 1,
