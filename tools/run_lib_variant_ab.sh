@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 P=scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd
 mkdir -p /tmp/var
 make -s -C $P/csrc -j16 >/dev/null || exit 1
-make -s -C $P/csrc -j16 BUILD=/tmp/var/build OUT=/tmp/var/libgpscore.so EXTRA="$1" >/dev/null || exit 1
+make -s -C $P/csrc -j16 GPS_BUILD_DIR=/tmp/var/build GPS_LIB_OUT=/tmp/var/libgpscore.so GPS_EXTRA_FLAGS="$1" >/dev/null || exit 1
 for v in base var; do
   L=$PWD/$P/gpscore; [ $v = var ] && L=/tmp/var
   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I$P/csrc -Iinclude tools/gemm_bench.cpp \
