@@ -16,8 +16,8 @@ fit (Gram + Cholesky + L⁻¹ + α + diag(A⁻¹) → NLML, LOO-CRPS, LOO-LogS) 
   recorded on the library's stream over the timed region; ``roofline_gram`` the
   HBM-bound Gram kernel.
 * ``cpu_baseline``: the oracle's ref-mirror restatement of the reference op
-  sequence (oracle/gp_oracle.py, numpy/LAPACK, all threads) on a bounded C2-size
-  sample, extrapolated O(n³) to C3; rank 0 at N = 1 only.
+  sequence (oracle/gp_oracle.py, numpy/LAPACK, all threads) timed on one full C3
+  unit (~1 min on the box's 16 host threads); rank 0 at N = 1 only.
 
 Inputs are synthetic (SURVEY.md §8d generator) and resident in HBM before the
 timed region.  Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -186,22 +186,24 @@ def roofline_gram(prof, steps=1, traffic=None, tags=("gram_kff", "gram_ksf")):
 
 
 def cpu_baseline():
-    """ref-mirror oracle (reference op sequence) on C2, extrapolated to C3."""
+    """ref-mirror oracle (the reference op sequence) on the full C3 workload, one unit.
+
+    Timed directly rather than extrapolated: C2 × 64 (O(n³)) overstated the C3 time 2.6×
+    on the MI355X box host (151 s vs 57.5 s measured, profiles/r1h_cpu_c3_direct.json) —
+    host BLAS runs much closer to peak at n = 20 000 than at 5 000."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import gp_oracle as O
-    c = CONFIGS["C2"]
+    c = CONFIGS["C3"]
     X, y, Xt, yt, _, th = synth(c["n"], c["d"], c["nt"], c["seed"])
     t0 = time.perf_counter()
     O.ref_full(X, y, Xt, yt, *th)
     t = time.perf_counter() - t0
-    scale = (CONFIGS["C3"]["n"] / c["n"]) ** 3
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": 1.0 / (t * scale), "unit": "fit+predict+score units/s (C3, extrapolated)",
+    return {"value": 1.0 / t, "unit": "fit+predict+score units/s (C3)",
             "cores": cores, "kind": "port",
             "sample": f"oracle ref_full (reference op sequence: upper potrf + 2 LU solves per "
-                      f"chol_solve, full n*×n* cov) on C2 n={c['n']} d={c['d']} n*={c['nt']}: "
-                      f"{t:.2f} s, ×{scale:.0f} (O(n³), n and n* both ×4) → C3 "
-                      f"{t * scale:.1f} s/unit"}
+                      f"chol_solve, full n*×n* cov) on the full C3 workload n={c['n']} "
+                      f"d={c['d']} n*={c['nt']}, one unit: {t:.1f} s"}
 
 
 def main():
