@@ -216,12 +216,6 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-grad", action="store_true")
     ap.add_argument("--no-block", action="store_true", help="skip the block-LOO (next-2) leg")
-    ap.add_argument("--lookahead", type=int, default=0,
-                    help="recursion depths with a split (lookahead) trailing update; 0 disables")
-    ap.add_argument("--reserve-cus", type=int, default=None,
-                    help="CUs kept free of the off-critical-path streams (library default 16)")
-    ap.add_argument("--fused-splitk", action="store_true",
-                    help="in-launch split-K combine instead of the separate reduce kernel")
     ap.add_argument("--no-tiny-gemm", action="store_true",
                     help="64-tile split-K path for the small GEMMs instead of the 16x16-per-wave kernel")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -234,13 +228,8 @@ def main():
     ctl = Ctl(world)
     import gpscore
     ctx = gpscore.Context(0 if args.rehearse else local)
-    ctx.set_lookahead(args.lookahead)
-    if args.fused_splitk:
-        ctx.set_fused_splitk(True)
     if args.no_tiny_gemm:
         ctx.set_tiny_gemm(False)
-    if args.reserve_cus is not None:
-        ctx.set_reserved_cus(args.reserve_cus)
     gp = gpscore.GP(ctx=ctx)
 
     # ---------------- full GP (replicas) ----------------

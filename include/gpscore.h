@@ -60,35 +60,23 @@ int gps_ctx_set_stream(gps_ctx* ctx, void* hip_stream);
 void* gps_ctx_stream(gps_ctx* ctx);
 int gps_ctx_synchronize(gps_ctx* ctx);
 
-/* ---- options ---------------------------------------------------------------- */
+/* ---- options ----------------------------------------------------------------
+ * Only options the defaults use.  Round-1 experiments measured neutral or slower on C3
+ * (lookahead split, CU-reserved streams, in-launch split-K combine, CU-masked main stream,
+ * split-K fill of the trailing update) were removed from the library. */
 enum {
-  GPS_OPT_OVERLAP = 0,  /* 1 (default): off-critical-path GEMMs of the factorisation run on
-                           extra HIP streams; 0: everything on one stream (clean per-kernel timing) */
-  GPS_OPT_LOOKAHEAD = 1, /* recursion depths (0..2, default 0) whose trailing update is split so
-                           the child's leading block is factored while the rest is updated */
-  GPS_OPT_RESERVE_CUS = 2, /* CUs (default 0) the off-critical-path streams may not use (CU-masked
-                           streams; measured slower on MI355X, kept for experiments) */
-  GPS_OPT_GEMM_MAP = 3,   /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
-  GPS_OPT_FORK_MIN = 4,   /* smallest recursion block (in 128-row blocks, default 1) whose
-                             off-critical-path product is forked to the side stream */
-  GPS_OPT_FUSED_SPLITK = 5, /* 1: split-K GEMM slabs are combined inside the launch by the
-                             last-arriving slice (agent-scope release/acquire ticket); 0 (default,
-                             measured faster on C3): a separate ordered reduce kernel.  Same
-                             numerics either way. */
-  GPS_OPT_TINY_GEMM = 7,   /* 1 (default): GEMMs with M·N <= 256² and K <= 1024 (the bottom of
-                             the recursion) use the one-wave-per-16×16-tile kernel; 0: 64-tile
-                             split-K + reduce.  Process-wide. */
-  GPS_OPT_MAIN_CU_EXCLUDE = 6, /* recreate the context's own main stream CU-masked so that the
-                             top `value` CU ids (r/8 per XCD) stay free for other streams/
-                             contexts (0 = unmasked, the default).  For co-scheduling studies. */
-  GPS_OPT_SYRK_SPLIT = 8,  /* 1: the factorisation's trailing updates with >= one full round
-                             of 128-tiles split K (1..4 slices) to fill the last round of
-                             resident workgroups; 0 (default, measured faster end-to-end on
-                             C3 because the overlap streams already fill it): one launch.  Same numerics up to
-                             the order of the K summation (deterministic either way). */
-  GPS_OPT_GRAM_REG = 9,    /* 1 (default): Gram builds with d in {1, 8, 16} keep the column
-                             features in registers (128×128 tiles); 0: the LDS-column kernel.
-                             Bitwise-identical output.  Process-wide. */
+  GPS_OPT_OVERLAP = 0,  /* 1 (default): the factorisation's off-critical-path products (and the
+                           energy score's folds) run on extra HIP streams; 0: everything on one
+                           stream (clean per-kernel timing) */
+  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
+  GPS_OPT_FORK_MIN = 4, /* smallest recursion block (in 128-row blocks, default 1) whose
+                           off-critical-path product is forked to the side stream */
+  GPS_OPT_TINY_GEMM = 7, /* 1 (default): GEMMs with M·N <= 256² and K <= 1024 (the bottom of
+                            the recursion) use the one-wave-per-16×16-tile kernel; 0: 64-tile
+                            split-K + reduce.  Process-wide. */
+  GPS_OPT_GRAM_REG = 9,  /* 1 (default): Gram builds with d in {1, 8, 16} keep the column
+                            features in registers (128×128 tiles); 0: the LDS-column kernel.
+                            Bitwise-identical output.  Process-wide. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
@@ -199,6 +187,13 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
 /* ---- multi-GPU (RCCL over xGMI) ------------------------------------------- */
 int gps_comm_unique_id(char uid[128]);
 int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]);
+/* In-process stand-in for the communicator: nranks contexts of ONE process (each driven by its
+ * own host thread, e.g. several shards on one GPU) that pass the same `group` key meet at every
+ * all-reduce of the FITC path, where their partials are summed on the host in rank order.
+ * Same call sites and element counts as the RCCL path; used to test the row-sharded FITC
+ * bookkeeping without a multi-GPU node (a rank that waits > 300 s returns an error). */
+int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group);
+/* Leaves either communicator. */
 int gps_comm_destroy(gps_ctx* ctx);
 
 #ifdef __cplusplus

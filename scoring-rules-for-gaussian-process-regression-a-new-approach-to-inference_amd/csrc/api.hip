@@ -23,9 +23,13 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -54,6 +58,23 @@ struct Theta {
   double inv_ell[GPS_MAX_D];
 };
 
+// In-process stand-in for the RCCL communicator (gps_comm_init_local): nranks contexts of one
+// process, each driven by its own host thread, meet at every all-reduce of the row-sharded
+// FITC path; the partials are summed on the host in rank order and written back.  Same call
+// sites and extents as ncclAllReduce, so the shard bookkeeping is exercised on one GPU.
+struct LocalGroup {
+  std::mutex mu;
+  std::condition_variable cv;
+  int n = 0, arrived = 0;
+  uint64_t gen = 0;
+  size_t count = 0;
+  bool mismatch = false, last_mismatch = false;
+  std::vector<std::vector<double>> in;
+  std::vector<double> sum;
+};
+std::mutex g_groups_mu;
+std::map<long long, std::weak_ptr<LocalGroup>> g_groups;
+
 }  // namespace
 
 struct gps_ctx {
@@ -61,17 +82,9 @@ struct gps_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = true;
   hipStream_t side = nullptr;          // second stream for off-critical-path GEMMs
-  hipStream_t look[2] = {nullptr, nullptr};  // lookahead trailing updates, recursion depth 0 / 1
+  hipStream_t aux[2] = {nullptr, nullptr};  // two more streams (concurrent energy-score folds)
   bool overlap = true;                 // GPS_OPT_OVERLAP
-  int lookahead = 0;                   // GPS_OPT_LOOKAHEAD: recursion depths with a split update
-                                       // (measured neutral on C3: 131.2 vs 130.1 ms; off by default)
-  int reserve_cus = 0;                 // GPS_OPT_RESERVE_CUS: CUs kept free of off-path streams
   int gemm_map = 0;                    // GPS_OPT_GEMM_MAP: tile-order override (A/B measurements)
-  int fused_splitk = 0;                // GPS_OPT_FUSED_SPLITK: split-K slabs combined in-launch by
-                                       // the last-arriving slice.  Measured slower on C3 (142.1 vs
-                                       // 135.9 ms same box): the last slice reads ks x 32 KB of
-                                       // slabs serially at the cross-XCD rate, ~4 us per tile,
-                                       // more than the reduce launch it removes.  Off by default.
   int fork_min = 1;                    // GPS_OPT_FORK_MIN: smallest n1 (in 128-blocks) whose T GEMM
                                        // goes to the side stream (a fork/join costs ~13 us, but
                                        // forking every level measured best: 128.3 vs 129.1 ms)
@@ -115,15 +128,14 @@ struct gps_ctx {
   double f_ytr_mean = 0, f_ytr_var = 1;
   bool f_data = false, f_test = false, f_z = false, f_fitted = false;
   Theta fth;
-  // ---- comm
+  // ---- comm: RCCL (gps_comm_init) or the in-process group (gps_comm_init_local)
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LocalGroup> lgroup;
   int nranks = 1, rank = 0;
   // ---- compat scratch (gps_gram / potrf / potrs / diag_inv / scores)
   DBuf t0, t1, t2, t3, t4;
   // ---- split-K slabs, one per stream (GEMMs on different streams run concurrently)
-  DBuf ws_main, ws_side, ws_look[2];
-  DBuf ws_syrk;                        // split-K slabs of the trailing update (syrk_splits)
-  int syrk_split = 0;                  // GPS_OPT_SYRK_SPLIT: 1 fill-model split-K, 0 off (default: C3 A/B 130.5 vs 129.6 ms)
+  DBuf ws_main, ws_side, ws_aux[2];
 };
 
 namespace {
@@ -259,16 +271,12 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
   // the stream's slabs: gemm_plan may split K on small grids; an explicit 64-tile split uses them
   if (epi == EPI_STORE && (q.ksplit == 1 || q.tile == 64) && !q.ws) {
     DBuf& ws = st == ctx->side      ? ctx->ws_side
-               : st == ctx->look[0] ? ctx->ws_look[0]
-               : st == ctx->look[1] ? ctx->ws_look[1]
-                                    : ctx->ws_main;
-    if (ws.cap < (size_t)kSplitWsDoubles * 8 + GPS_SPLITK_TICKETS * 4) {
-      HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8 + GPS_SPLITK_TICKETS * 4));
-      HIPCHK(hipMemsetAsync(ws.d() + kSplitWsDoubles, 0, GPS_SPLITK_TICKETS * 4, st));
-    }
+               : st == ctx->aux[0] ? ctx->ws_aux[0]
+               : st == ctx->aux[1] ? ctx->ws_aux[1]
+                                   : ctx->ws_main;
+    HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8));
     q.ws = ws.d();
     q.ws_cap = kSplitWsDoubles;
-    q.cnt = ctx->fused_splitk ? reinterpret_cast<unsigned*>(ws.d() + kSplitWsDoubles) : nullptr;
   }
   std::string tag = gemm_tag(al, bl, epi, p);
   if (ctx->prof > 1) {  // per-shape accounting (gps_prof_enable(ctx, 2))
@@ -308,45 +316,21 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
   return 0;
 }
 
-// Split-K of the trailing update A22 −= L21 L21ᵀ.  Its lower 128-tiles all carry the same
-// K, so a grid that is not a whole number of rounds of resident workgroups (2 per CU) idles
-// the last round: 3160 tiles at the C3 top level are 6.17 rounds of 512.  Take ks in 1..4
-// maximising the filled fraction of the last round, 1 % off per extra slice for the slab
-// traffic, keeping >= 512 of K per slice.  tools/gemm_bench syrk (MI355X): 10112², K = 9984
-// 60.2 → 65.4 / 66.7 / 67.2 TF/s at ks 2 / 3 / 4; 5120² 53.5 → 62.4 at ks 3; 4992² 51.5 → 59.8.
-int syrk_splits(int64_t tiles, int slots, int K) {
-  int best = 1;
-  double best_score = 0.0;
-  for (int ks = 1; ks <= 4 && K / ks >= 512; ++ks) {
-    const double x = (double)tiles * ks / slots;
-    const double score = x / std::ceil(x) * (1.0 - 0.01 * (ks - 1));
-    if (score > best_score + 1e-9) {
-      best_score = score;
-      best = ks;
-    }
-  }
-  return best;
-}
-
 // recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
 // W is this level's workspace (n1·n2 doubles); deeper levels on the A22 side get
 // the region after it, so a concurrent GEMM that still reads this level's W never
 // races with them.
 //
-// Streams (when ctx->overlap):
-//  * T = L21 L11⁻¹ only feeds the final L⁻¹21 product, so it runs off the main
-//    stream (fork / join events) concurrently with the trailing update and rec(A22);
-//  * lookahead (depth < ctx->lookahead): of the trailing update A22 -= W Wᵀ only the
-//    child's leading block B11 is on the main stream; B21 / B22 are updated on
-//    look[depth] while the child factors B11 (its latency-bound leaves leave most
-//    CUs idle).  The child waits for that update (`pending`) just before it reads
-//    its own A21.  T of a lookahead level queues behind the update on the same stream.
+// T = L21 L11⁻¹ only feeds the final L⁻¹21 product, so (ctx->overlap) it runs on the
+// side stream (fork / join events) concurrently with the trailing update and rec(A22).
+// Measured on C3 and dropped from the build (round 1): a lookahead split of the trailing
+// update, CU-masked side streams and split-K fill of the top-level SYRK — each neutral or
+// slower end to end, because the side stream's T product already fills the idle slots.
 int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
                   int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
-                  int64_t ldlo, int depth, hipEvent_t pending) {
+                  int64_t ldlo) {
   hipStream_t s = ctx->stream;
   if (nb == 1) {
-    if (pending) HIPCHK(hipStreamWaitEvent(s, pending, 0));
     Prof pr(ctx, "potrf_diag128", 2.0 * 128 * 128 * 128 / 3.0, 0);
     HIPCHK(launch_potrf_diag(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, s));
     return 0;
@@ -358,10 +342,8 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   double* Li21 = Linv + (int64_t)n1 * ldl;
   double* Li22 = Li21 + n1;
   int rc;
-  if ((rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo,
-                          depth + 1, nullptr)))
+  if ((rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo)))
     return rc;
-  if (pending) HIPCHK(hipStreamWaitEvent(s, pending, 0));  // parent's lookahead update of A21/A22
   {  // W = L21 = A21 · L11⁻ᵀ
     GemmParams p = gp0();
     p.A = A21; p.lda = lda; p.B = Linv; p.ldb = ldl; p.C = W; p.ldc = n1;
@@ -370,52 +352,20 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   }
   if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
                                     (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
-  const bool look = ctx->overlap && depth < ctx->lookahead && n2b >= 2;
-  // an event fork + join costs ~13 us of dependent-chain latency (tools/launch_latency.hip),
-  // more than the overlap wins for the small T products near the leaves
-  const bool forked = ctx->overlap && (look || n1b >= ctx->fork_min);
-  hipStream_t ts = !forked ? s : (look ? ctx->look[depth] : ctx->side);
-  hipEvent_t fork = sync_event(ctx), join = sync_event(ctx), upd = nullptr;
+  // an event fork + join costs ~13 us of dependent-chain latency (tools/launch_latency.hip)
+  const bool forked = ctx->overlap && n1b >= ctx->fork_min;
+  hipStream_t ts = forked ? ctx->side : s;
+  hipEvent_t fork = sync_event(ctx), join = sync_event(ctx);
   if (!fork || !join) return fail(ctx, -2, "hipEventCreate failed");
   if (forked) {
     HIPCHK(hipEventRecord(fork, s));
     HIPCHK(hipStreamWaitEvent(ts, fork, 0));
   }
-  // trailing update A22 -= L21 L21ᵀ (lower tiles); with lookahead split at the child's
-  // split point m1: B11 on the main stream, B21 and B22 on ts
-  const int m1 = look ? (n2b / 2) * GPS_TILE : n2;
-  {
+  {  // trailing update A22 -= L21 L21ᵀ (lower tiles)
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
-    p.M = m1; p.N = m1; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
-    const int64_t tiles = (int64_t)(m1 / GPS_TILE) * (m1 / GPS_TILE + 1) / 2;
-    const int ks = ctx->syrk_split && tiles >= 2 * ctx->ncu ? syrk_splits(tiles, 2 * ctx->ncu, n1)
-                                                             : 1;
-    if (ks > 1) {
-      HIPCHK(ensure(ctx->ws_syrk, (size_t)ks * m1 * m1 * 8));
-      p.tile = GPS_TILE; p.ksplit = ks; p.ws = ctx->ws_syrk.d();
-      p.ws_cap = (int64_t)(ctx->ws_syrk.cap / 8);
-    }
+    p.M = n2; p.N = n2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
-  }
-  if (look) {
-    const int m2 = n2 - m1;
-    const double* W2 = W + (int64_t)m1 * n1;
-    {  // B21 -= W2 W1ᵀ
-      GemmParams p = gp0();
-      p.A = W2; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22 + (int64_t)m1 * lda; p.ldc = lda;
-      p.M = m2; p.N = m1; p.K = n1; p.alpha = -1.0; p.beta = 1.0;
-      if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p, ts))) return rc;
-    }
-    {  // B22 -= W2 W2ᵀ
-      GemmParams p = gp0();
-      p.A = W2; p.lda = n1; p.B = W2; p.ldb = n1; p.C = A22 + (int64_t)m1 * lda + m1; p.ldc = lda;
-      p.M = m2; p.N = m2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
-      if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p, ts))) return rc;
-    }
-    upd = sync_event(ctx);
-    if (!upd) return fail(ctx, -2, "hipEventCreate failed");
-    HIPCHK(hipEventRecord(upd, ts));
   }
   {  // T = L21 · L11⁻¹ → A21 (off the critical path)
     GemmParams p = gp0();
@@ -426,7 +376,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   if (forked) HIPCHK(hipEventRecord(join, ts));
   if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W + (int64_t)n1 * n2, n2b, logdiag + n1, info,
                           base + n1, nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr,
-                          ldlo, depth + 1, upd)))
+                          ldlo)))
     return rc;
   if (forked) HIPCHK(hipStreamWaitEvent(s, join, 0));
   {  // L⁻¹21 = −L22⁻¹ · T
@@ -460,7 +410,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
               int nreal, double* Lout) {
   ctx->sync_used = 0;
   int rc = potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
-                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad, 0, nullptr);
+                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad);
   return rc;
 }
 
@@ -514,6 +464,53 @@ int bind(gps_ctx* ctx) {
     return -1;
   }
   HIPCHK(hipSetDevice(ctx->device));
+  return 0;
+}
+
+bool sharded(const gps_ctx* ctx) { return ctx->comm != nullptr || ctx->lgroup != nullptr; }
+
+// Σ over the ranks of `count` doubles at buf (device, in place, stream s): ncclAllReduce on
+// the RCCL communicator, or the in-process group's host sum; a no-op on one rank.
+int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
+  if (ctx->comm) {
+    NCCLCHK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, ctx->comm, s));
+    return 0;
+  }
+  if (!ctx->lgroup) return 0;
+  LocalGroup& G = *ctx->lgroup;
+  std::vector<double> mine(count);
+  HIPCHK(hipMemcpyAsync(mine.data(), buf, count * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<double> out;
+  bool bad;
+  {
+    std::unique_lock<std::mutex> lk(G.mu);
+    if (G.arrived == 0) {
+      G.count = count;
+      G.mismatch = false;
+    } else if (G.count != count) {
+      G.mismatch = true;
+    }
+    G.in[ctx->rank] = std::move(mine);
+    const uint64_t my = G.gen;
+    if (++G.arrived == G.n) {
+      G.sum.assign(G.count, 0.0);
+      for (int r = 0; r < G.n; ++r)  // rank order: deterministic
+        for (size_t i = 0; i < std::min(G.count, G.in[r].size()); ++i) G.sum[i] += G.in[r][i];
+      G.last_mismatch = G.mismatch;
+      G.arrived = 0;
+      ++G.gen;
+      G.cv.notify_all();
+    } else if (!G.cv.wait_for(lk, std::chrono::seconds(300), [&] { return G.gen != my; })) {
+      return fail(ctx, -3, "local all-reduce: timed out waiting for the other ranks");
+    }
+    out = G.sum;
+    bad = G.last_mismatch;
+  }
+  if (bad || out.size() != count)
+    return fail(ctx, -3, "local all-reduce: ranks passed different element counts");
+  HIPCHK(hipMemcpyAsync(buf, out.data(), count * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
 
@@ -826,7 +823,7 @@ int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const doub
     if (want_grad && (rc = gdone(f, a, b))) return rc;
   }
   if (es_conc) {
-    hipStream_t st[4] = {s, ctx->side, ctx->look[0], ctx->look[1]};
+    hipStream_t st[4] = {s, ctx->side, ctx->aux[0], ctx->aux[1]};
     DBuf* eb[4] = {&ctx->ebuf, &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2]};
     const int nst = std::min(nfold, 4);
     hipEvent_t fork = sync_event(ctx);
@@ -876,30 +873,11 @@ extern "C" {
 
 int gps_version(void) { return 100; }
 
-// (re)create the off-critical-path streams (side, look[]) with a CU mask that leaves
-// reserve_cus CUs, spread evenly over the device, to the main stream: a concurrent
-// big GEMM holds every workgroup slot with ~1 ms tiles, which would otherwise stall the
-// main stream's latency-bound chain (diag-block kernels need a whole CU's LDS).
+// the off-critical-path streams: side (T products of the factorisation) and aux[0..1]
+// (with side, the concurrent energy-score folds)
 int make_aux_streams(gps_ctx* ctx) {
-  HIPCHK(hipDeviceSynchronize());
-  if (ctx->side) HIPCHK(hipStreamDestroy(ctx->side));
-  for (hipStream_t& l : ctx->look)
-    if (l) HIPCHK(hipStreamDestroy(l));
-  ctx->side = nullptr;
-  ctx->look[0] = ctx->look[1] = nullptr;
-  const int ncu = ctx->ncu, r = std::min(ctx->reserve_cus, ncu / 2);
-  std::vector<hipStream_t*> aux = {&ctx->side, &ctx->look[0], &ctx->look[1]};
-  if (r <= 0) {
-    for (hipStream_t* a : aux) HIPCHK(hipStreamCreateWithFlags(a, hipStreamNonBlocking));
-    return 0;
-  }
-  // CU ids interleave over the XCDs (id % 8 on MI355X: a stride-16 mask that removed
-  // one XCD's CUs halved the masked streams' throughput under in-order dispatch), so the
-  // top r ids take r/8 CUs from every XCD
-  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu - r; ++i) mask[i / 32] |= 1u << (i % 32);
-  for (hipStream_t* a : aux)
-    HIPCHK(hipExtStreamCreateWithCUMask(a, (uint32_t)mask.size(), mask.data()));
+  for (hipStream_t* a : {&ctx->side, &ctx->aux[0], &ctx->aux[1]})
+    HIPCHK(hipStreamCreateWithFlags(a, hipStreamNonBlocking));
   return 0;
 }
 
@@ -938,17 +916,17 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
                  &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
-                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_look[0], &ctx->ws_look[1],
+                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_aux[0], &ctx->ws_aux[1],
                  &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
-                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws, &ctx->ws_syrk,
+                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
                  &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW};
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
-  for (hipStream_t l : ctx->look)
+  for (hipStream_t l : ctx->aux)
     if (l) (void)hipStreamDestroy(l);
   if (ctx->hsmall) (void)hipHostFree(ctx->hsmall);
   if (ctx->hinfo) (void)hipHostFree(ctx->hinfo);
@@ -977,30 +955,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
   if (int rc = bind(ctx)) return rc;
   switch (key) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
-    case GPS_OPT_LOOKAHEAD: ctx->lookahead = value < 0 ? 0 : (value > 2 ? 2 : value); return 0;
     case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
-    case GPS_OPT_FUSED_SPLITK: ctx->fused_splitk = value != 0; return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
-    case GPS_OPT_SYRK_SPLIT: ctx->syrk_split = value != 0; return 0;
-    case GPS_OPT_MAIN_CU_EXCLUDE: {  // recreate the (owned) main stream CU-masked
-      ARGCHK(ctx->own_stream, "the main stream is caller-owned");
-      HIPCHK(hipStreamSynchronize(ctx->stream));
-      HIPCHK(hipStreamDestroy(ctx->stream));
-      const int ncu = ctx->ncu, r = std::max(0, std::min(value, ncu / 2));
-      if (r == 0) {
-        HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-      } else {
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu - r; ++i) mask[i / 32] |= 1u << (i % 32);
-        HIPCHK(hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mask.size(), mask.data()));
-      }
-      return 0;
-    }
-    case GPS_OPT_RESERVE_CUS:
-      ctx->reserve_cus = value < 0 ? 0 : value;
-      return make_aux_streams(ctx);
     default: return fail(ctx, -1, "unknown option");
   }
 }
@@ -1255,6 +1213,7 @@ int gps_full_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t 
 // Gram + factorisation + β, α, diag(A⁻¹) + LOO sums; objectives land in ctx->small (device)
 int full_fit_core(gps_ctx* ctx, int kind, const double* theta, int n_ell) {
   ARGCHK(ctx->have_data, "gps_full_set_data first");
+  ctx->fitted = false;  // set again only once the factor is known to be PD (check_info)
   if (int rc = set_theta(ctx, ctx->th, kind, theta, n_ell, ctx->d)) return rc;
   ctx->n_ell = n_ell;
   const int64_t n = ctx->n, np = ctx->n_pad;
@@ -1504,7 +1463,10 @@ int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m) {
 // in whole rounds of 512 slots (2 per CU): take the smallest split whose last round is
 // >= 95 % full (528 tiles at m = 4096: ks 3 -> 77 % of the slots busy on average, ks 12
 // -> 95 %), with at least 1024 rows per slice and at most 32 slabs.
-int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* dst) {
+// With `packed` the sum goes lower-packed (m(m+1)/2, launch_sym_pack) into dst instead: the
+// all-reduce payload of the row-sharded path (base must be NULL then).
+int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* dst,
+              bool packed = false) {
   const int64_t np = ctx->fn_pad, mp = ctx->m_pad, tm = mp / GPS_TILE;
   const int64_t tiles_lower = tm * (tm + 1) / 2;
   int ks = 1;
@@ -1521,13 +1483,17 @@ int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* ds
   p.lower_out = 1; p.ksplit = ks;
   if (int rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p)) return rc;
   Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * mp * mp);
-  HIPCHK(launch_sym_slab_sum(ctx->slabB.d(), mp * mp, ks, (int)mp, base, dst, ctx->stream));
+  if (packed)
+    HIPCHK(launch_sym_pack(ctx->slabB.d(), mp * mp, ks, (int)ctx->m, (int)mp, dst, ctx->stream));
+  else
+    HIPCHK(launch_sym_slab_sum(ctx->slabB.d(), mp * mp, ks, (int)mp, base, dst, ctx->stream));
   return 0;
 }
 
 // forward FITC objectives; leaves Knm, Lm⁻¹, Lb⁻¹, λ, r, g = Knm c, c on the device
 int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ]) {
   ARGCHK(ctx->f_data && ctx->f_z, "gps_fitc_set_data / gps_fitc_set_inducing first");
+  ctx->f_fitted = false;  // set again by the callers once check_info has passed
   if (int rc = set_theta(ctx, ctx->fth, GPS_ARD, theta, n_ell, ctx->fd)) return rc;
   const Theta& th = ctx->fth;
   const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
@@ -1557,6 +1523,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   HIPCHK(ensure(ctx->fvar_loo, np * 8));
   HIPCHK(ensure(ctx->c, mp * 8));
   HIPCHK(ensure(ctx->tvec, mp * 8));
+  // all-reduce buffer [B | b | scalars]: B lower-packed (m(m+1)/2) when the rows are sharded,
+  // the padded lower tiles (m_pad²) on one rank
+  const bool shard = sharded(ctx);
+  const int64_t blen = shard ? m * (m + 1) / 2 : mp * mp;
   const int64_t red_len = mp * mp + mp + 8;
   HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
   const int64_t nchunk = (std::max(np, mp) + 255) / 256;
@@ -1564,8 +1534,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   HIPCHK(ensure(ctx->fslab, (size_t)fslab_len * 8));
   double* red = ctx->red.d();
   double* Bacc = red;
-  double* bvec = red + mp * mp;
-  double* scal = red + mp * mp + mp;  // [Σlogλ, Σy²/λ, Σcrps, Σlogs]
+  double* bvec = red + blen;
+  double* scal = bvec + mp;  // [Σlogλ, Σy²/λ, Σcrps, Σlogs]
   double* sm = ctx->small.d();        // [logdet_m/2, logdet_b/2, bᵀc]
   int rc;
   if ((rc = reset_info(ctx))) return rc;
@@ -1595,18 +1565,21 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                               ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal, s));
   }
   // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs)
-  if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc))) return rc;
+  if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc, shard))) return rc;
   {  // b_p = Kmnᵀ Λ⁻¹ y
     Prof pr(ctx, "colred_b", 0, 8.0 * np * mp);
     HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ctx->ys.d(), nullptr, bvec,
                          nullptr, ctx->fslab.d(), s));
   }
-  if (ctx->comm) {
-    Prof pr(ctx, "rccl_allreduce_B", 0, 8.0 * (mp * mp + mp + 2));
-    NCCLCHK(ncclAllReduce(red, red, (size_t)(mp * mp + mp + 2), ncclFloat64, ncclSum, ctx->comm, s));
+  if (shard) {  // ONE all-reduce: B packed, b, Σlogλ, Σy²/λ
+    Prof pr(ctx, "allreduce_B", 0, 8.0 * (blen + mp + 2));
+    if ((rc = allreduce_sum(ctx, red, (size_t)(blen + mp + 2), s))) return rc;
   }
   // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
-  HIPCHK(launch_sym_slab_sum(Bacc, 0, 1, (int)mp, ctx->Kmm.d(), ctx->Am.d(), s));
+  if (shard)
+    HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
+  else
+    HIPCHK(launch_sym_slab_sum(Bacc, 0, 1, (int)mp, ctx->Kmm.d(), ctx->Am.d(), s));
   if ((rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr)))
     return rc;
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
@@ -1631,7 +1604,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n,
                            ctx->fmu_loo.d(), ctx->fvar_loo.d(), scal + 2, s));
   }
-  if (ctx->comm) NCCLCHK(ncclAllReduce(scal + 2, scal + 2, 2, ncclFloat64, ncclSum, ctx->comm, s));
+  if ((rc = allreduce_sum(ctx, scal + 2, 2, s))) return rc;
   HIPCHK(hipMemcpyAsync(ctx->hsmall, scal, 4 * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(ctx->hsmall + 4, sm, 3 * 8, hipMemcpyDeviceToHost, s));
   if ((rc = check_info(ctx))) return rc;
@@ -1690,7 +1663,8 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   // scratch
   HIPCHK(ensure(ctx->fgv, (size_t)11 * np * 8));
   HIPCHK(ensure(ctx->fgm, (size_t)6 * mp * 8));
-  HIPCHK(ensure(ctx->fgB, (size_t)5 * mp * mp * 8));
+  const bool shard = sharded(ctx);
+  HIPCHK(ensure(ctx->fgB, (size_t)(shard ? 6 : 5) * mp * mp * 8));
   HIPCHK(ensure(ctx->fR, (size_t)np * 3 * mp * 8));
   HIPCHK(ensure(ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
   const int passes = fitc_contract_passes(d);
@@ -1707,9 +1681,19 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   double* Bb = ctx->fgB.d();
   double *Binv = Bb, *Kminv = Bb + mp * mp, *Nm = Bb + 2 * mp * mp, *T1 = Bb + 3 * mp * mp,
          *KmD = Bb + 4 * mp * mp;
-  double* red = ctx->fgred.d();  // [m×m SYRK | Kᵀv (mp) | Σ M_ii | ...]
-  double* tw = red + mp * mp;
-  double* smd = red + mp * mp + mp;
+  // all-reduce buffer [P | Σ M_ii | (pad) | Kᵀv (mp)]: P an m×m SYRK, lower-packed (m(m+1)/2)
+  // when the rows are sharded, else the padded lower tiles (m_pad²)
+  const int64_t plen = shard ? m * (m + 1) / 2 : mp * mp;
+  const int64_t off_tw = (plen + 2) / 2 * 2;  // 16-byte aligned
+  double* red = ctx->fgred.d();
+  double* smd = red + plen;
+  double* tw = red + off_tw;
+  double* Sfull = shard ? Bb + 5 * mp * mp : red;  // the reduced P, both triangles
+  auto sym_full = [&]() -> int {
+    if (shard) HIPCHK(launch_sym_unpack(red, (int)m, (int)mp, nullptr, 1, Sfull, s));
+    else HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
+    return 0;
+  };
   double* out1 = ctx->fgout.d();        // Knm contraction [passes*17 | m*d]
   double* out2 = out1 + outlen;         // Kmm contraction
   double* R = ctx->fR.d();
@@ -1729,19 +1713,19 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   if (loo) {  // v = C⁻¹u = u/λ − (K B⁻¹ Kᵀ(u/λ))/λ
     HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr,
                          ctx->fslab.d(), s));
-    if (ctx->comm) NCCLCHK(ncclAllReduce(tku, tku, (size_t)mp, ncclFloat64, ncclSum, ctx->comm, s));
+    if ((rc = allreduce_sum(ctx, tku, (size_t)mp, s))) return rc;
     HIPCHK(launch_gemv_full(Binv, mp, tku, tbt, (int)mp, (int)mp, s));
     HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, tbt, zv, (int)np, (int)mp, s));
     HIPCHK(launch_fitc_grad_v(ulam, zv, ctx->lam.d(), (int)n, v, s));
     // S2 = Kᵀ diag(h/λ²) K
-    if ((rc = fitc_syrk(ctx, hl2, nullptr, red))) return rc;
+    if ((rc = fitc_syrk(ctx, hl2, nullptr, red, shard))) return rc;
   }
   HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, v, nullptr, tw, nullptr,
                        ctx->fslab.d(), s));  // Kᵀv
-  if (ctx->comm) {
+  {  // LOO: [S2 | (Σ M_ii, not yet formed) | Kᵀv] in one call; NLML: Kᵀv.  Kᵀv is final here.
     double* r0 = loo ? red : tw;
-    const size_t cnt = loo ? (size_t)(mp * mp + mp) : (size_t)mp;
-    NCCLCHK(ncclAllReduce(r0, r0, cnt, ncclFloat64, ncclSum, ctx->comm, s));
+    const size_t cnt = loo ? (size_t)(off_tw + mp) : (size_t)mp;
+    if ((rc = allreduce_sum(ctx, r0, cnt, s))) return rc;
   }
   HIPCHK(launch_gemv_full(Kminv, mp, tw, what, (int)mp, (int)mp, s));  // ŵ = Km⁻¹Kᵀv
   auto gemm_nn = [&](const double* A, int64_t lda, const double* B, double* C, int64_t ldc,
@@ -1752,8 +1736,8 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
     return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
   };
   if (loo) {  // N = B⁻¹ S2 B⁻¹
-    HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
-    if ((rc = gemm_nn(red, mp, Binv, T1, mp, (int)mp))) return rc;
+    if ((rc = sym_full())) return rc;
+    if ((rc = gemm_nn(Sfull, mp, Binv, T1, mp, (int)mp))) return rc;
     if ((rc = gemm_nn(Binv, mp, T1, Nm, mp, (int)mp))) return rc;
   }
   // R = K·[B⁻¹ | N | Km⁻¹]
@@ -1767,12 +1751,11 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
                                   (int)n, (int)np, md, s1, s2, s3, s));
   }
   // Kᵀ diag(M_ii) K and Σ M_ii (this shard) → all-reduce
-  if ((rc = fitc_syrk(ctx, md, nullptr, red))) return rc;
+  if ((rc = fitc_syrk(ctx, md, nullptr, red, shard))) return rc;
   HIPCHK(launch_dot(md, nullptr, (int)np, smd, s));
-  if (ctx->comm)
-    NCCLCHK(ncclAllReduce(red, red, (size_t)(mp * mp + mp + 1), ncclFloat64, ncclSum, ctx->comm, s));
-  HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
-  if ((rc = gemm_nn(red, mp, Kminv, T1, mp, (int)mp))) return rc;
+  if ((rc = allreduce_sum(ctx, red, (size_t)(plen + 1), s))) return rc;  // [P | Σ M_ii], not Kᵀv
+  if ((rc = sym_full())) return rc;
+  if ((rc = gemm_nn(Sfull, mp, Kminv, T1, mp, (int)mp))) return rc;
   if ((rc = gemm_nn(Kminv, mp, T1, KmD, mp, (int)mp))) return rc;
   // contraction with ∂Knm/∂θ, ∂Knm/∂Z
   FitcContractParams cp;
@@ -1792,8 +1775,7 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
     Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * (loo ? 3 : 2) * np * mp);
     HIPCHK(launch_fitc_grad_contract(p, out1, out1 + passes * 17, s));
   }
-  if (ctx->comm)
-    NCCLCHK(ncclAllReduce(out1, out1, (size_t)outlen, ncclFloat64, ncclSum, ctx->comm, s));
+  if ((rc = allreduce_sum(ctx, out1, (size_t)outlen, s))) return rc;
   {  // ∂Km/∂θ, ∂Km/∂Z (replicated on every rank; jitter is a constant)
     FitcContractParams p = cp;
     p.xr = ctx->Z.d(); p.xc = ctx->Z.d(); p.nr = (int)m; p.nc = (int)m; p.nc_pad = (int)mp;
@@ -1845,7 +1827,6 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
                          double* fold_values) {
   int rc;
   if ((rc = full_fit_core(ctx, kind, theta, n_ell))) return rc;
-  ctx->fitted = true;
   const int64_t n = ctx->n, np = ctx->n_pad;
   ARGCHK(n >= nfold, "fewer rows than folds");
   hipStream_t s = ctx->stream;
@@ -1878,6 +1859,7 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
                            grad != nullptr, gdst, gdone, grad ? ctx->gu.d() : nullptr, es,
                            fv.data())))
     return rc;
+  ctx->fitted = true;  // blockloo_folds checked the main factor (check_info)
   double tot = 0.0;
   for (int f = 0; f < nfold; ++f) tot += fv[f];
   *value = tot;
@@ -2046,7 +2028,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   ARGCHK(objective == GPS_BLOCK_DSS || objective == GPS_BLOCK_KC,
          "objective must be GPS_BLOCK_DSS or GPS_BLOCK_KC");
   ARGCHK(value != nullptr, "value is NULL");
-  ARGCHK(ctx->comm == nullptr, "FITC block-LOO needs every row on one rank");
+  ARGCHK(!sharded(ctx), "FITC block-LOO needs every row on one rank");
   double o[GPS_N_OBJ];
   int rc;
   if ((rc = fitc_fit_core(ctx, theta, n_ell, o))) return rc;
@@ -2293,7 +2275,7 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
     else
       HIPCHK(hipMemsetAsync(sums, 0, 6 * 8, s));
   }
-  if (ctx->comm) NCCLCHK(ncclAllReduce(sums, sums, 6, ncclFloat64, ncclSum, ctx->comm, s));
+  if (int rc2 = allreduce_sum(ctx, sums, 6, s)) return rc2;
   HIPCHK(hipMemcpyAsync(ctx->hsmall, sums, 6 * 8, hipMemcpyDeviceToHost, s));
   if (mu && nt) HIPCHK(hipMemcpyAsync(mu, ctx->fmu.p, nt * 8, hipMemcpyDeviceToHost, s));
   if (var && nt) HIPCHK(hipMemcpyAsync(var, ctx->fvar.p, nt * 8, hipMemcpyDeviceToHost, s));
@@ -2319,9 +2301,32 @@ int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]) {
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  ctx->lgroup.reset();
   ncclUniqueId id;
   memcpy(&id, uid, 128);
   NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return 0;
+}
+
+int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(nranks >= 1 && rank >= 0 && rank < nranks, "bad communicator arguments");
+  if (ctx->comm) {
+    ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_groups_mu);
+  std::shared_ptr<LocalGroup> G = g_groups[group].lock();
+  if (!G) {
+    G = std::make_shared<LocalGroup>();
+    G->n = nranks;
+    G->in.resize(nranks);
+    g_groups[group] = G;
+  }
+  ARGCHK(G->n == nranks, "local group: nranks differs from the group's");
+  ctx->lgroup = G;
   ctx->nranks = nranks;
   ctx->rank = rank;
   return 0;
@@ -2331,6 +2336,7 @@ int gps_comm_destroy(gps_ctx* ctx) {
   if (int rc = bind(ctx)) return rc;
   if (ctx->comm) NCCLCHK(ncclCommDestroy(ctx->comm));
   ctx->comm = nullptr;
+  ctx->lgroup.reset();
   ctx->nranks = 1;
   ctx->rank = 0;
   return 0;

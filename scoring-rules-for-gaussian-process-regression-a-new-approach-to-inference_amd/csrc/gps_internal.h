@@ -11,7 +11,6 @@
 
 #define GPS_TILE 128
 #define GPS_MAX_D 64
-#define GPS_SPLITK_TICKETS 16384
 
 namespace gps {
 
@@ -66,10 +65,6 @@ struct GemmParams {
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
-  unsigned* cnt;             // split-K tile tickets (>= GPS_SPLITK_TICKETS, zeroed): the slice
-                             // that draws ksplit-1 sums the slabs in slice order (in-launch)
-  // in-launch combine target (set by launch_gemm): C = alpha_f * Σ slabs + beta_f * C
-  double* Cf; int64_t ldcf; double alpha_f, beta_f;
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
@@ -170,6 +165,13 @@ hipError_t launch_slab_sum(const double* slab, int64_t ld, int nslab, int64_t le
 hipError_t launch_sym_slab_sum(const double* slab, int64_t slice_stride, int nslab, int M,
                                const double* base, double* dst, hipStream_t s);
 
+// symmetric m×m accumulator <-> lower-packed m(m+1)/2 (the FITC all-reduce payload):
+// packed = Σ_q slab_q (lower, row-major);  dst (M×M) = base + unpack(packed), lower 128-tiles
+// (strict-upper tiles zero) or, with full, both triangles
+hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, int m, int M,
+                           double* packed, hipStream_t s);
+hipError_t launch_sym_unpack(const double* packed, int m, int M, const double* base, int full,
+                             double* dst, hipStream_t s);
 // full-GP LOO finalize (one workgroup): see kernels_vec.hip
 hipError_t launch_full_loo(const double* y, const double* alpha, const double* dinv,
                            const double* beta, const double* logdiag, int n,

@@ -274,45 +274,6 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
           crow[ni * 16] = v;
         }
       }
-    if (p.cnt) {
-      // in-launch split-K combine (cdna_hip_programming.md, projection-GEMM item 2): publish
-      // this slice's slab with an agent-scope release, draw a ticket; the slice that draws
-      // ksplit-1 acquires and sums all slabs in slice order (bitwise the same result as the
-      // separate reduce kernel, whatever the arrival order or XCD placement).
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      unsigned* flag = reinterpret_cast<unsigned*>(smem);
-      const int tlin = blockIdx.x;
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(p.cnt + tlin, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned last = t == (unsigned)(p.ksplit - 1);
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(p.cnt + tlin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        flag[0] = last;
-      }
-      __syncthreads();
-      if (flag[0] == 0u) return;
-      const int64_t slab = p.c_kslice_stride;
-      constexpr int PAIRS = TILE * TILE / 2 / 256;
-#pragma unroll 4
-      for (int q = 0; q < PAIRS; ++q) {
-        const int e = 2 * (q * 256 + tid);
-        const int row = row0 + e / TILE, col = col0 + e % TILE;
-        const double* src = p.C + (int64_t)row * p.ldc + col;
-        dv2 sum = *reinterpret_cast<const dv2*>(src);
-        for (int s = 1; s < p.ksplit; ++s) sum += *reinterpret_cast<const dv2*>(src + s * slab);
-        dv2* c = reinterpret_cast<dv2*>(p.Cf + (int64_t)row * p.ldcf + col);
-        dv2 v = p.alpha_f * sum;
-        if (p.beta_f != 0.0) v += p.beta_f * *c;
-        *c = v;
-      }
-    }
   } else if constexpr (EPI == EPI_ROWSQ) {
     // out0[tj][row] = sum over this tile's columns of (alpha*acc)^2
     double* red = smem;  // [2 (wc)][TILE rows]
@@ -545,12 +506,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     q.c_kslice_stride = (int64_t)p.M * p.N;
     q.alpha = 1.0;
     q.beta = 0.0;
-    q.Cf = p.C;
-    q.ldcf = p.ldc;
-    q.alpha_f = p.alpha;
-    q.beta_f = p.beta;
-  } else {
-    q.cnt = nullptr;
   }
   q.tiles_m = q.M / tile;
   q.tiles_n = q.N / tile;
@@ -564,7 +519,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
                                                           : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;
   }
-  if (q.cnt && tiles > GPS_SPLITK_TICKETS) q.cnt = nullptr;  // falls back to the reduce kernel
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
 #define GPS_GEMM_CASE(AL, BL, EP, T)                                               \
@@ -583,7 +537,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE, 64)
   GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE, 64)
 #undef GPS_GEMM_CASE
-  if (err != hipSuccess || !slabbed || q.cnt) return err;
+  if (err != hipSuccess || !slabbed) return err;
   const int64_t pairs = (int64_t)p.M * p.N / 2;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s,
                      p.ws, p.ksplit, p.M, p.N, p.lower_out ? tile : 0, p.alpha, p.beta, p.C, p.ldc);

@@ -1,26 +1,9 @@
 // Diagonal-block kernel of the blocked Cholesky (replaces LAPACK ?potrf behind
 // torch.potrf, KF:26 / KF:332) fused with the block's triangular inverse.
 //
-// One 1024-thread workgroup owns a 128×128 fp64 block.  Thread t holds the 4×4
-// sub-block (br, bc) = (t >> 5, t & 31) in registers; only the 528 lower
-// sub-blocks do arithmetic.  The block is processed in 32 panel steps of width 4:
-//
-//   factor, step jb (two barriers):
-//     1. thread (jb, jb) factors its 4×4 diagonal block in registers (one
-//        rsqrt per pivot, no divisions: this is the serial critical path),
-//        inverts it (D⁻¹), records the first non-positive pivot (torch.potrf's
-//        "leading minor not PD"), and publishes L_jj and D⁻¹ to LDS;
-//     2. the panel threads (br > jb, bc = jb) form L_rb = A_rb D⁻ᵀ and publish it;
-//     3. every trailing thread (br >= bc > jb) applies the rank-4 update
-//        A_rc -= L_rb L_cbᵀ from LDS.  The diagonal thread of step jb+1 finishes
-//        its own update first and factors immediately (natural look-ahead).
-//   invert, step ib (one barrier): X = L⁻¹ by block forward substitution on
-//     X = I held in the same registers: block row ib is finalised
-//     X_ib ← D_ib⁻¹ X_ib and published, then every block row r > ib does
-//     X_r -= L_r,ib X_ib.
-// log L_ii (the ½log|A| terms of KF:332) is taken for all 128 pivots in parallel
-// after the factorisation.  L is kept transposed in LDS (LT[col][row], 132-double rows) so a thread's
-// 4-row slice of an L column is one contiguous 32-byte read.
+// One 640-thread workgroup owns a 128×128 fp64 block held as 4×4 sub-blocks in
+// registers; log L_ii (the ½log|A| terms of KF:332) is taken for all 128 pivots in
+// parallel after the factorisation.  Details at potrf_diag_v3_kernel.
 #include "gps_internal.h"
 
 namespace gps {
@@ -34,223 +17,8 @@ __device__ __forceinline__ void lds_read4(const double* p, double (&v)[4]) {
   v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
 }
 
-#ifdef GPS_DIAG_STAMPS
-__device__ unsigned long long gps_stamps[32 * 8 * 17];
-#endif
-#ifdef GPS_V3_STAMPS
-__device__ unsigned long long gps_stamps3[32 * 8];
-#endif
-
-__global__ __launch_bounds__(1024) void potrf_diag_kernel(const double* __restrict__ A, int64_t lda,
-                                                          double* __restrict__ Linv, int64_t ldl,
-                                                          double* __restrict__ Lout, int64_t ldlo,
-                                                          double* __restrict__ logdiag, int* info,
-                                                          int base, int nreal) {
-  __shared__ __attribute__((aligned(16))) double LT[NB * LTS];   // LT[col][row] = L[row][col]
-  __shared__ __attribute__((aligned(16))) double DI[32 * 16];    // D_b⁻¹ (4×4, row-major) per block
-  __shared__ __attribute__((aligned(16))) double XB[2 * 4 * NB]; // published X block row [4][128]
-  const int tid = threadIdx.x;
-  const int br = tid >> 5, bc = tid & 31;
-  const bool lower = bc <= br;
-  const int r0 = br * 4, c0 = bc * 4;
-
-  double a[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (lower) {
-      const double2* src = reinterpret_cast<const double2*>(A + (int64_t)(r0 + r) * lda + c0);
-      const double2 u = src[0], v = src[1];
-      a[r][0] = u.x; a[r][1] = u.y; a[r][2] = v.x; a[r][3] = v.y;
-    } else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a[r][c] = 0.0;
-    }
-  }
-
-#ifndef GPS_DIAG_ABLATE
-#define GPS_DIAG_ABLATE 0  // tools/diag_bench.cpp: 1 skip pivot math, 2 skip updates, 3 skip inverse
-#endif
-#ifdef GPS_DIAG_STAMPS
-#define STAMP(slot)                                                                    \
-  do {                                                                                 \
-    __builtin_amdgcn_sched_barrier(0);                                                 \
-    unsigned long long _t;                                                             \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
-    __builtin_amdgcn_sched_barrier(0);                                                 \
-    if ((tid & 63) == 0 || tid == 33 * jb) gps_stamps[(jb * 8 + (slot)) * 17 + (tid == 33 * jb ? 16 : (tid >> 6))] = _t; \
-  } while (0)
-#else
-#define STAMP(slot) do {} while (0)
-#endif
-  // ======================= factorisation =======================
-  for (int jb = 0; jb < 32; ++jb) {
-    STAMP(0);
-    if (br == jb && bc == jb && GPS_DIAG_ABLATE != 1) {
-      // 4×4 Cholesky in registers: one rsqrt per pivot, no divisions on this
-      // serial path (it is the per-step critical path of the whole block)
-      double is[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const double d = a[j][j];
-        if (!(d > 0.0) && 4 * jb + j < nreal) atomicMin(info, base + 4 * jb + j + 1);
-        is[j] = rsqrt(d);
-        a[j][j] = d * is[j];
-#pragma unroll
-        for (int r = j + 1; r < 4; ++r) a[r][j] *= is[j];
-#pragma unroll
-        for (int r = j + 1; r < 4; ++r)
-#pragma unroll
-          for (int c = j + 1; c <= r; ++c) a[r][c] = fma(-a[r][j], a[c][j], a[r][c]);
-      }
-      // D⁻¹ by forward substitution, x_rc = -(1/L_rr) Σ_{c<=k<r} L_rk x_kc, x_cc = 1/L_cc
-      double x[4][4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (r < c) {
-            x[r][c] = 0.0;
-          } else if (r == c) {
-            x[r][c] = is[r];
-          } else {
-            double t = 0.0;
-#pragma unroll
-            for (int k = c; k < r; ++k) t = fma(a[r][k], x[k][c], t);
-            x[r][c] = -t * is[r];
-          }
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          DI[jb * 16 + r * 4 + c] = x[r][c];
-          LT[(c0 + c) * LTS + r0 + r] = (c <= r) ? a[r][c] : 0.0;
-        }
-    }
-    STAMP(1);
-    __syncthreads();
-    STAMP(2);
-    if (lower && bc == jb && br > jb) {  // panel: L_rb = A_rb D⁻ᵀ
-      double di[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) lds_read4(&DI[jb * 16 + r * 4], di[r]);
-      double l[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double s = 0.0;
-#pragma unroll
-          for (int k = 0; k <= c; ++k) s = fma(a[r][k], di[c][k], s);
-          l[r][c] = s;
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          a[r][c] = l[r][c];
-          LT[(c0 + c) * LTS + r0 + r] = l[r][c];
-        }
-    }
-    STAMP(3);
-    __syncthreads();
-    STAMP(4);
-    if (lower && bc > jb && GPS_DIAG_ABLATE != 2) {  // trailing rank-4 update
-      double lr[4][4], lc[4][4];  // [k][r]
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        lds_read4(&LT[(4 * jb + k) * LTS + r0], lr[k]);
-        lds_read4(&LT[(4 * jb + k) * LTS + c0], lc[k]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double s = a[r][c];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) s = fma(-lr[k][r], lc[k][c], s);
-          a[r][c] = s;
-        }
-    }
-  }
-  __syncthreads();
-  if (tid < NB) logdiag[tid] = log(LT[tid * LTS + tid]);
-
-  if (Lout) {
-    for (int e = tid; e < NB * NB / 2; e += 1024) {
-      const int r = e >> 6, c = (e & 63) * 2;
-      const double v0 = c <= r ? LT[c * LTS + r] : 0.0;
-      const double v1 = c + 1 <= r ? LT[(c + 1) * LTS + r] : 0.0;
-      *reinterpret_cast<double2*>(Lout + (int64_t)r * ldlo + c) = make_double2(v0, v1);
-    }
-  }
-
-  // ======================= X = L⁻¹ =======================
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) a[r][c] = (r0 + r == c0 + c) ? 1.0 : 0.0;
-
-  for (int ib = 0; ib < (GPS_DIAG_ABLATE == 3 ? 0 : 32); ++ib) {
-    double* xb = XB + (ib & 1) * 4 * NB;
-    if (lower && br == ib) {  // X_ib ← D_ib⁻¹ X_ib, publish
-      double di[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) lds_read4(&DI[ib * 16 + r * 4], di[r]);
-      double x[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double s = 0.0;
-#pragma unroll
-          for (int k = 0; k <= r; ++k) s = fma(di[r][k], a[k][c], s);
-          x[r][c] = s;
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) a[r][c] = x[r][c];
-        *reinterpret_cast<double2*>(&xb[r * NB + c0]) = make_double2(x[r][0], x[r][1]);
-        *reinterpret_cast<double2*>(&xb[r * NB + c0 + 2]) = make_double2(x[r][2], x[r][3]);
-      }
-    }
-    __syncthreads();
-    if (lower && br > ib && bc <= ib) {  // X_r -= L_r,ib X_ib
-      double lr[4][4], xi[4][4];  // lr[k][r] = L[r0+r][4ib+k]; xi[k][c] = X[4ib+k][c0+c]
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        lds_read4(&LT[(4 * ib + k) * LTS + r0], lr[k]);
-        lds_read4(&xb[k * NB + c0], xi[k]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double s = a[r][c];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) s = fma(-lr[k][r], xi[k][c], s);
-          a[r][c] = s;
-        }
-    }
-  }
-
-  // write L⁻¹ (explicit zeros above the diagonal)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    double v[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = (lower && c0 + c <= r0 + r) ? a[r][c] : 0.0;
-    double2* dst = reinterpret_cast<double2*>(Linv + (int64_t)(r0 + r) * ldl + c0);
-    dst[0] = make_double2(v[0], v[1]);
-    dst[1] = make_double2(v[2], v[3]);
-  }
-}
-
-
 // ---------------------------------------------------------------------------
-// v3: the 528 lower 4×4 blocks are packed column-major into 10 waves, every
+// the 528 lower 4×4 blocks are packed column-major into 10 waves, every
 // block column inside ONE wave (wave w owns columns [kColStart[w], kColStart[w+1])).
 //
 //   factor, step jb (one barrier):
@@ -323,27 +91,11 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
     }
   }
 
-#ifndef GPS_V3_ABLATE
-#define GPS_V3_ABLATE 0  // tools/diag_bench.cpp: 1 no inverse, 2 no trailing update, 4 no factor loop
-#endif
-#ifdef GPS_V3_STAMPS  // tools/diag_bench.cpp: per-phase s_memtime of the wave owning column jb
-#define S3(slot)                                                                        \
-  do {                                                                                  \
-    __builtin_amdgcn_sched_barrier(0);                                                  \
-    unsigned long long _t;                                                              \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
-    __builtin_amdgcn_sched_barrier(0);                                                  \
-    if (lane == 0) gps_stamps3[jb * 8 + (slot)] = _t;                                   \
-  } while (0)
-#else
-#define S3(slot) do {} while (0)
-#endif
   // ======================= factorisation =======================
-  for (int jb = 0; jb < ((GPS_V3_ABLATE & 4) ? 0 : 32); ++jb) {
+  for (int jb = 0; jb < 32; ++jb) {
     const bool mine = w == wave_of_col(jb);  // wave-uniform
-    if (mine) S3(0);
     if (mine) __builtin_amdgcn_s_setprio(2);
-    if (jb > 0 && active && bc >= jb && !(GPS_V3_ABLATE & 2)) {  // a. rank-4 update, L column jb-1
+    if (jb > 0 && active && bc >= jb) {  // a. rank-4 update, L column jb-1
       const double* cb = CB + ((jb - 1) & 1) * 4 * NB;
       double lr[4][4], lc[4][4];  // [k][i]
 #pragma unroll
@@ -362,7 +114,6 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
         }
     }
     if (mine) {  // b. pivot (redundantly in every lane of this wave) + panel
-      S3(1);
       int ljj = 0;
       for (int c = cs; c < jb; ++c) ljj += 32 - c;
       ljj = __builtin_amdgcn_readfirstlane(ljj);
@@ -401,7 +152,6 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
             x[r][c] = -t * is[r];
           }
         }
-      S3(2);
       double* cb = CB + (jb & 1) * 4 * NB;
       if (active && bc == jb && br > jb) {  // panel: L_rj = A_rj D⁻ᵀ, kept in a[][]
         double L[4][4];                     // L[r][c] = Σ_{k<=c} a[r][k] x[c][k]
@@ -424,19 +174,15 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
 #pragma unroll
           for (int c = 0; c < 4; ++c) a[r][c] = L[r][c];
       }
-      S3(3);
       if (lane == ljj) {  // the diagonal block's own lane keeps L_jj (D⁻¹ is rebuilt after the loop)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int c = 0; c < 4; ++c) a[r][c] = c <= r ? l[r][c] : 0.0;
       }
-      S3(4);
-      S3(5);
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
-    if (mine) S3(6);
   }
   // ---- off the per-step critical path: D⁻¹ and L_jj of every diagonal block (in parallel)
   if (active && br == bc) {
@@ -519,7 +265,7 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
 #pragma unroll
     for (int c = 0; c < 4; ++c) a[r][c] = (active && br == bc && r == c) ? 1.0 : 0.0;
   double* xr = XR + w * 7 * 16;
-  for (int k = cs; k < ((GPS_V3_ABLATE & 1) ? 0 : 31); ++k) {
+  for (int k = cs; k < 31; ++k) {
     if (active && br == k) {  // publish R_k,c (final: every update from rows < k applied)
       double* dst = xr + (bc - cs) * 16;
 #pragma unroll
@@ -581,13 +327,8 @@ hipError_t launch_potrf_diag(const double* A, int64_t lda, double* Linv, int64_t
                              int64_t ldlo, double* logdiag, int* info, int base, int nreal,
                              hipStream_t s) {
   if ((lda & 1) || (ldl & 1) || (Lout && (ldlo & 1))) return hipErrorInvalidValue;
-#ifdef GPS_DIAG_V1
-  hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(1024), 0, s, A, lda, Linv, ldl, Lout, ldlo,
-                     logdiag, info, base, nreal);
-#else
   hipLaunchKernelGGL(potrf_diag_v3_kernel, dim3(1), dim3(64 * V3_WAVES), 0, s, A, lda, Linv, ldl,
                      Lout, ldlo, logdiag, info, base, nreal);
-#endif
   return hipGetLastError();
 }
 

@@ -152,6 +152,60 @@ hipError_t launch_sym_slab_sum(const double* slab, int64_t slice_stride, int nsl
   return hipGetLastError();
 }
 
+// Lower-packed form of a symmetric m×m accumulator (row i holds columns 0..i at offset
+// i(i+1)/2): the payload of the FITC row-shard all-reduce, m(m+1)/2 doubles instead of
+// the padded m_pad².  Pack sums the split-K slabs in slice order (the
+// same sums sym_slab_sum forms); unpack adds the optional base and writes either the
+// lower 128-tiles (strict-upper tiles zero, as sym_slab_sum) or the full symmetric matrix.
+__global__ __launch_bounds__(256) void sym_pack_kernel(const double* __restrict__ slab,
+                                                       int64_t stride, int nslab, int m, int M,
+                                                       double* __restrict__ packed) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t len = (int64_t)m * (m + 1) / 2;
+  if (e >= len) return;
+  int i = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+  while ((int64_t)(i + 1) * (i + 2) / 2 <= e) ++i;
+  while ((int64_t)i * (i + 1) / 2 > e) --i;
+  const int j = (int)(e - (int64_t)i * (i + 1) / 2);
+  const int64_t src = (int64_t)i * M + j;
+  double v = 0.0;
+  for (int q = 0; q < nslab; ++q) v += slab[(int64_t)q * stride + src];
+  packed[e] = v;
+}
+
+__global__ __launch_bounds__(256) void sym_unpack_kernel(const double* __restrict__ packed, int m,
+                                                         int M, const double* __restrict__ base,
+                                                         int full, double* __restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)M * M) return;
+  const int i = (int)(e / M), j = (int)(e - (int64_t)i * M);
+  double v = 0.0;
+  if (full || j / GPS_TILE <= i / GPS_TILE) {
+    if (i < m && j < m) {
+      const int hi = i > j ? i : j, lo = i > j ? j : i;
+      v = packed[(int64_t)hi * (hi + 1) / 2 + lo];
+    }
+    if (base) v += base[e];
+  }
+  dst[e] = v;
+}
+
+hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, int m, int M,
+                           double* packed, hipStream_t s) {
+  const int64_t len = (int64_t)m * (m + 1) / 2;
+  hipLaunchKernelGGL(sym_pack_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, slab,
+                     slice_stride, nslab, m, M, packed);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_unpack(const double* packed, int m, int M, const double* base, int full,
+                             double* dst, hipStream_t s) {
+  const int64_t tot = (int64_t)M * M;
+  hipLaunchKernelGGL(sym_unpack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                     packed, m, M, base, full, dst);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ full-GP LOO
 // obj: [nlml, loo_crps, loo_logs, logdet, quad]; logdiag/beta over n_pad (pad = 0)
 __global__ __launch_bounds__(1024) void full_loo_kernel(const double* __restrict__ y,

@@ -17,9 +17,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
-GPS_OPT_OVERLAP, GPS_OPT_LOOKAHEAD, GPS_OPT_RESERVE_CUS, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN = 0, 1, 2, 3, 4
-GPS_OPT_FUSED_SPLITK, GPS_OPT_MAIN_CU_EXCLUDE, GPS_OPT_TINY_GEMM, GPS_OPT_SYRK_SPLIT = 5, 6, 7, 8
-GPS_OPT_GRAM_REG = 9
+GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
@@ -65,6 +63,7 @@ SIGNATURES = {
     "gps_fitc_predict": (_c_int, [_c_vp, _P, _P, _P]),
     "gps_comm_unique_id": (_c_int, [_c_cp]),
     "gps_comm_init": (_c_int, [_c_vp, _c_int, _c_int, _c_cp]),
+    "gps_comm_init_local": (_c_int, [_c_vp, _c_int, _c_int, ctypes.c_longlong]),
     "gps_comm_destroy": (_c_int, [_c_vp]),
 }
 
@@ -165,18 +164,6 @@ class Context:
         """Run the factorisation's off-critical-path GEMMs on a second stream."""
         self.call("gps_ctx_set_option", GPS_OPT_OVERLAP, 1 if on else 0)
 
-    def set_lookahead(self, depth=0):
-        """Recursion depths whose trailing update is split for lookahead (0 disables)."""
-        self.call("gps_ctx_set_option", GPS_OPT_LOOKAHEAD, int(depth))
-
-    def set_reserved_cus(self, n=16):
-        """CUs the off-critical-path streams may not use (recreates those streams)."""
-        self.call("gps_ctx_set_option", GPS_OPT_RESERVE_CUS, int(n))
-
-    def set_fused_splitk(self, on=True):
-        """In-launch split-K combine, or the separate ordered reduce kernel (default)."""
-        self.call("gps_ctx_set_option", GPS_OPT_FUSED_SPLITK, 1 if on else 0)
-
     def set_tiny_gemm(self, on=True):
         """One-wave-per-16×16 kernel for the small GEMMs at the bottom of the recursion
         (default) or the 64-tile split-K path (process-wide)."""
@@ -186,11 +173,6 @@ class Context:
         """Register-resident Gram kernel for d in {1, 8, 16} (default) or the LDS-column
         kernel; bitwise-identical output (process-wide)."""
         self.call("gps_ctx_set_option", GPS_OPT_GRAM_REG, 1 if on else 0)
-
-    def set_syrk_split(self, on=True):
-        """Fill-model split-K for the factorisation's big trailing updates, or one launch
-        each (default)."""
-        self.call("gps_ctx_set_option", GPS_OPT_SYRK_SPLIT, 1 if on else 0)
 
     def synchronize(self):
         self.call("gps_ctx_synchronize")

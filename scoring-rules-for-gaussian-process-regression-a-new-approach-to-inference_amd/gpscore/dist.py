@@ -32,17 +32,20 @@ def shard_rows(n, nranks, rank):
 
 def global_target_stats(y_local, group=None):
     """(mean, unbiased var, n_total) of the training targets over all ranks —
-    what trivial_loss / SMSE need (KF:112-114, 130) — via one all-reduce of
-    [Σy, Σy², n] in float64 on the host (works with gloo or nccl groups)."""
+    what trivial_loss / SMSE need (KF:112-114, 130).  Two passes over float64 host
+    all-reduces (works with gloo or nccl groups): [Σy, n] gives the global mean, then
+    Σ(y − mean)² — no cancellation when the mean is large against the spread."""
     import torch
     import torch.distributed as dist
     y = np.asarray(y_local, dtype=np.float64).ravel()
     dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
-    t = torch.tensor([y.sum(), (y * y).sum(), float(y.size)], dtype=torch.float64, device=dev)
+    t = torch.tensor([y.sum(), float(y.size)], dtype=torch.float64, device=dev)
     dist.all_reduce(t, group=group)
-    s, s2, n = (float(v) for v in t.cpu())
+    s, n = (float(v) for v in t.cpu())
     mean = s / n
-    var = (s2 - n * mean * mean) / (n - 1) if n > 1 else 1.0
+    c = torch.tensor([float(((y - mean) ** 2).sum())], dtype=torch.float64, device=dev)
+    dist.all_reduce(c, group=group)
+    var = float(c.cpu()[0]) / (n - 1) if n > 1 else 1.0
     return mean, var, int(round(n))
 
 
@@ -89,6 +92,11 @@ class ShardedFITC:
 
     def set_data(self, X_full, y_full, Z, Xt_full=None, yt_full=None):
         n = len(y_full)
+        if n < self.world:
+            # every rank sees the same n, so every rank raises here — none is left inside
+            # an all-reduce waiting for a rank whose empty shard the library rejected
+            raise ValueError(f"{n} training rows cannot be sharded over {self.world} ranks "
+                             "(every rank needs at least one row)")
         a, b = shard_rows(n, self.world, self.rank)
         ytr_mean = float(np.mean(y_full))
         ytr_var = float(np.var(y_full, ddof=1))

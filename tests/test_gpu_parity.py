@@ -186,23 +186,20 @@ def test_c3_config_properties(gp):
 
 
 def test_stream_schedules_agree(gp, gpu_ctx):
-    """Lookahead (split trailing update on extra streams), side-stream overlap and the
-    single-stream schedule compute the same factorisation: only the split-K plan of
-    the split updates may change the summation grouping, so agreement is ~1e-13."""
+    """Side-stream overlap and the single-stream schedule compute the same factorisation
+    (the same launches in the same per-stream order): agreement to ~1e-13."""
     rng = np.random.default_rng(11)
     n, nt, d = 6016, 512, 8
     X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
     y, yt = np.sin(X.sum(1)), np.sin(Xt.sum(1))
     th = (0.0, np.log(1.5) * np.ones(d), np.log(0.01))
     runs = []
-    for overlap, look in ((True, 2), (True, 0), (False, 0)):
+    for overlap in (True, False):
         gpu_ctx.set_overlap(overlap)
-        gpu_ctx.set_lookahead(look)
         r = gp.fit(X, y, th)
         mu, var = gp.predict(Xt, yt)
         runs.append((r, mu, var))
-    gpu_ctx.set_overlap(True)
-    gpu_ctx.set_lookahead(0)  # library default
+    gpu_ctx.set_overlap(True)  # library default
     r0, mu0, var0 = runs[0]
     for r, mu, var in runs[1:]:
         assert nrel(r.mu_loo, r0.mu_loo) < 1e-11 and nrel(r.var_loo, r0.var_loo) < 1e-11
@@ -211,6 +208,40 @@ def test_stream_schedules_agree(gp, gpu_ctx):
             assert abs(r.objectives[k] - r0.objectives[k]) <= 1e-11 * max(1.0, abs(r0.objectives[k]))
     f = O.fast_full_fit(X, y, *th)
     assert nrel(r0.mu_loo, f["loo_mu"]) < 1e-9 and abs(r0.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
+
+
+def test_failed_fit_clears_factor(gpu_ctx):
+    """A fit that fails (non-PD / NaN factor) after a successful one leaves no stale factor
+    behind: predict then reports an error instead of returning numbers from the failed
+    attempt.  Full GP, block-LOO and FITC."""
+    import gpscore
+    rng = np.random.default_rng(2)
+    X, Xt = rng.standard_normal((400, 3)), rng.standard_normal((50, 3))
+    y = np.sin(X.sum(1))
+    good, bad = (0.0, 0.0, np.log(0.01)), (np.nan, 0.0, np.log(0.01))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    gp.set_data(X, y)
+    gp.set_test(Xt)
+    gp.fit(theta=good)
+    gp.predict()
+    with pytest.raises(gpscore.NotPositiveDefinite):
+        gp.fit(theta=bad)
+    with pytest.raises(gpscore.GpsError, match="fit first"):
+        gp.predict()
+    gp.fit(theta=good)
+    with pytest.raises(gpscore.NotPositiveDefinite):
+        gp.block_loo(bad, "dss")
+    with pytest.raises(gpscore.GpsError, match="fit first"):
+        gp.predict()
+    fg = gpscore.GP(ctx=gpu_ctx)
+    fg.set_data(X, y, kind="fitc", Z=X[:40])
+    fg.set_test(Xt)
+    fg.fit(theta=good)
+    fg.predict()
+    with pytest.raises(gpscore.NotPositiveDefinite):
+        fg.fit(theta=bad)
+    with pytest.raises(gpscore.GpsError, match="fit first"):
+        fg.predict()
 
 
 def test_not_positive_definite_raises(gp):
@@ -391,30 +422,3 @@ def test_profiler_collect(gpu_ctx):
     gpu_ctx.prof(False)
     assert "potrf_diag128" in rep and "gram_kff" in rep and "gemm_trmm_colred" in rep
     assert all(v["ms"] >= 0 for v in rep.values())
-
-
-def test_fused_splitk_bitwise(gpu_ctx):
-    """The in-launch split-K combine (agent-scope release/acquire ticket, last slice sums
-    the slabs in slice order) gives bitwise the same fit, predict and gradient as the
-    separate ordered reduce kernel: n = 3000 exercises split-K at every small recursion
-    level, repeated to shake out arrival orders."""
-    import gpscore
-    rng = np.random.default_rng(5)
-    n, nt, d = 3000, 700, 8
-    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
-    y = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n)
-    th = (0.0, np.log(np.linspace(1.0, 2.0, d)), np.log(0.01))
-    gp = gpscore.GP(ctx=gpu_ctx)
-    gp.set_data(X, y)
-    gp.set_test(Xt)
-    outs = []
-    for fused in (False, True, True, True):
-        gpu_ctx.set_fused_splitk(fused)
-        r = gp.fit(theta=th)
-        mu, var = gp.predict()
-        _, g, _ = gp.value_and_grad(th, "loo_crps")
-        outs.append((r.mu_loo, r.var_loo, mu, var, g))
-    gpu_ctx.set_fused_splitk(False)
-    for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert np.array_equal(a, b)

@@ -1,0 +1,136 @@
+"""Row-sharded FITC on ONE GPU: 2 and 3 shard contexts on device 0, each driven by its own
+host thread, joined by the in-process communicator (gps_comm_init_local).  Every all-reduce
+of the sharded path — the lower-packed B / b / scalar reduction of the forward, the LOO and
+test-score sums, the four gradient reductions — runs at the same call sites with the same
+element counts as under RCCL, with the partials summed on the host in rank order.  The
+sharded results must match the unsharded fit (K20:222-234, 270-296, 236/344/452).
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, nrel, theta_of
+
+pytestmark = pytest.mark.gpu
+
+OBJS = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
+_GROUP = [1000]
+
+
+def _case(n, nt, m, d, seed):
+    rng = np.random.default_rng(seed)
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
+    w = rng.standard_normal(d) / np.sqrt(d)
+    y = np.sin(3 * X @ w) + 0.1 * rng.standard_normal(n)
+    yt = np.sin(3 * Xt @ w) + 0.1 * rng.standard_normal(nt)
+    Z = X[rng.choice(n, m, replace=False)]
+    th = (0.1, np.log(np.linspace(1.6, 2.4, d)), np.log(0.02))
+    return X, y, Xt, yt, Z, th
+
+
+def _run(gp, th, with_grad):
+    r = gp.fit(theta=th)
+    mu, var, sc = gp.predict(with_scores=True)
+    out = {"obj": r.objectives, "mu_loo": r.mu_loo, "var_loo": r.var_loo, "mu": mu, "var": var,
+           "sc": sc}
+    if with_grad:
+        for o in ("nlml", "loo_crps", "loo_logs"):
+            _, g, objs = gp.value_and_grad(th, o)
+            out["g_" + o] = g
+            out["gz_" + o] = objs["grad_Z"]
+    return out
+
+
+def _sharded(P, X, y, Xt, yt, Z, th, with_grad):
+    import gpscore
+    from gpscore.dist import shard_rows
+    _GROUP[0] += 1
+    key = _GROUP[0]
+    n, nt = len(y), len(Xt)
+    stats = (float(y.mean()), float(y.var(ddof=1)))
+
+    def rank_job(r):
+        ctx = gpscore.Context(0)
+        try:
+            ctx.call("gps_comm_init_local", P, r, key)
+            gp = gpscore.GP(ctx=ctx)
+            a, b = shard_rows(n, P, r)
+            ta, tb = shard_rows(nt, P, r)
+            gp.set_data(X[a:b], y[a:b], kind="fitc", Z=Z, n_total=n, ytr_stats=stats)
+            gp.set_test(Xt[ta:tb], yt[ta:tb], nt_total=nt)
+            res = _run(gp, th, with_grad)
+            ctx.call("gps_comm_destroy")
+            return res
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(max_workers=P) as ex:
+        return list(ex.map(rank_job, range(P)))
+
+
+def _whole(X, y, Xt, yt, Z, th, with_grad, gpu_ctx):
+    import gpscore
+    gp = gpscore.GP(ctx=gpu_ctx)
+    gp.set_data(X, y, kind="fitc", Z=Z)
+    gp.set_test(Xt, yt)
+    return _run(gp, th, with_grad)
+
+
+def _compare(parts, ref, tol_obj, tol_vec, tol_grad):
+    for p in parts:  # global quantities: identical on every rank
+        for k in OBJS:
+            assert abs(p["obj"][k] - ref["obj"][k]) <= tol_obj * max(1.0, abs(ref["obj"][k])), k
+        for k, v in ref["sc"].items():
+            assert abs(p["sc"][k] - v) <= tol_obj * max(1.0, abs(v)), k
+        for k in ref:
+            if k.startswith("g"):
+                assert nrel(p[k], ref[k]) <= tol_grad, k
+    for k in ("mu_loo", "var_loo", "mu", "var"):  # row-sharded vectors, concatenated
+        assert nrel(np.concatenate([p[k] for p in parts]), ref[k]) <= tol_vec, k
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_fitc_shards_match_unsharded(gpu_ctx, P):
+    """n = 6001 (ragged shards), m = 300, d = 8: forward, predict, scores and the θ / Z
+    gradients of all three objectives."""
+    X, y, Xt, yt, Z, th = _case(6001, 1501, 300, 8, 41)
+    ref = _whole(X, y, Xt, yt, Z, th, True, gpu_ctx)
+    parts = _sharded(P, X, y, Xt, yt, Z, th, True)
+    _compare(parts, ref, 1e-12, 1e-11, 1e-10)
+
+
+def test_fitc_shards_golden(gpu_ctx):
+    """The reference-pinned golden case, 3 shards: same objectives as the dense reference."""
+    g = load_golden("fitc_n2000_m200_rows")
+    th, _ = theta_of(g)
+    parts = _sharded(3, g["X"], g["y"], g["Xt"], g["yt"], g["Z"], th, False)
+    for p in parts:
+        for k in ("nlml", "loo_crps", "loo_logs"):
+            assert abs(p["obj"][k] - float(g[k])) <= 1e-8 * max(1.0, abs(float(g[k]))), k
+    assert nrel(np.concatenate([p["mu_loo"] for p in parts]), g["loo_mu"]) < 1e-8
+    assert nrel(np.concatenate([p["mu"] for p in parts]), g["pred_mu"]) < 1e-8
+
+
+def test_fitc_shards_empty_test_shard(gpu_ctx):
+    """nt_total = 2 over 3 ranks leaves one rank without test rows; its zero score partials
+    still join the all-reduce and the global scores are those of the unsharded predict."""
+    X, y, Xt, yt, Z, th = _case(900, 2, 60, 4, 43)
+    ref = _whole(X, y, Xt, yt, Z, th, False, gpu_ctx)
+    parts = _sharded(3, X, y, Xt, yt, Z, th, False)
+    _compare(parts, ref, 1e-12, 1e-11, 1e-10)
+
+
+def test_block_loo_refuses_shards(gpu_ctx):
+    """FITC block-LOO needs all rows on one rank; a sharded context reports it (no hang)."""
+    import gpscore
+    X, y, Xt, yt, Z, th = _case(400, 10, 30, 3, 44)
+    ctx = gpscore.Context(0)
+    try:
+        ctx.call("gps_comm_init_local", 1, 0, 999999)
+        gp = gpscore.GP(ctx=ctx)
+        gp.set_data(X, y, kind="fitc", Z=Z)
+        with pytest.raises(gpscore.GpsError):
+            gp.block_loo(th, "kc")
+    finally:
+        ctx.close()

@@ -129,3 +129,39 @@ def test_compat_empty_inputs_follow_torch():
     assert np.isnan(compat.crps(e, e, e)) and np.isnan(compat.logs(e, e, e))
     assert np.isnan(compat.trivial_loss(e, e, e, np.ones(3)))
     assert np.isnan(compat.SMSE(e, e, np.ones(3)))
+
+
+def _stats_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gpscore.dist import ShardedFITC, global_target_stats, shard_rows
+    rng = np.random.default_rng(3)
+    y = 1e8 + rng.standard_normal(1001)  # mean far above the spread
+    a, b = shard_rows(len(y), world, rank)
+    mean, var, n = global_target_stats(y[a:b])
+
+    class _StubGP:  # a communicator already attached: no library call before the check
+        comm = (world, rank)
+
+    raised = False
+    try:
+        ShardedFITC(_StubGP()).set_data(np.zeros((world - 1, 2)), np.zeros(world - 1), None)
+    except ValueError:
+        raised = True
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), mean=mean, var=var, n=n, raised=raised)
+    dist.destroy_process_group()
+
+
+def test_target_stats_and_empty_shards_world2(tmp_path):
+    """global_target_stats is two-pass (a 1e8 offset does not cancel the variance away), and
+    fewer training rows than ranks raises on EVERY rank before any shard reaches the library
+    (an empty shard used to leave the other ranks waiting in the all-reduce)."""
+    world = 2
+    mp.spawn(_stats_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    y = 1e8 + np.random.default_rng(3).standard_normal(1001)
+    for r in range(world):
+        z = np.load(tmp_path / f"s{r}.npz")
+        assert abs(float(z["mean"]) - y.mean()) < 1e-7
+        assert abs(float(z["var"]) - y.var(ddof=1)) < 1e-9 * y.var(ddof=1)
+        assert int(z["n"]) == y.size and bool(z["raised"])

@@ -1,9 +1,8 @@
 """Same-box A/B of library schedule options on a bench workload (MI355X boxes differ by
 ~5% in GEMM clocks, so variants must be compared inside one run).
 
-  python tools/ab_bench.py --config C3 la=2,map=0 la=0,map=0 la=2,map=4
-  options: la (GPS_OPT_LOOKAHEAD), map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN),
-  syrk (GPS_OPT_SYRK_SPLIT)
+  python tools/ab_bench.py --config C3 map=0 map=4 ov=0
+  options: map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN)
 Variants are interleaved round-robin for --rounds rounds; prints the median ms/unit.
 """
 import argparse
@@ -21,8 +20,7 @@ import bench  # noqa: E402
 import gpscore  # noqa: E402
 from gpscore import _lib  # noqa: E402
 
-KEYS = {"la": _lib.GPS_OPT_LOOKAHEAD, "map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP,
-        "fork": _lib.GPS_OPT_FORK_MIN, "syrk": _lib.GPS_OPT_SYRK_SPLIT}
+KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN}
 
 
 def main():
