@@ -69,6 +69,7 @@ struct LocalGroup {
   uint64_t gen = 0;
   size_t count = 0;
   bool mismatch = false, last_mismatch = false;
+  bool aborted = false;  // a member left (comm destroy / context destroy): waits fail at once
   std::vector<std::vector<double>> in;
   std::vector<double> sum;
 };
@@ -469,6 +470,18 @@ int bind(gps_ctx* ctx) {
 
 bool sharded(const gps_ctx* ctx) { return ctx->comm != nullptr || ctx->lgroup != nullptr; }
 
+// A member leaving marks the group aborted: ranks waiting in (or later entering) one of
+// its all-reduces fail at once instead of waiting for a rank that will never arrive.
+void leave_local_group(gps_ctx* ctx) {
+  if (!ctx->lgroup) return;
+  {
+    std::lock_guard<std::mutex> lk(ctx->lgroup->mu);
+    ctx->lgroup->aborted = true;
+  }
+  ctx->lgroup->cv.notify_all();
+  ctx->lgroup.reset();
+}
+
 // Σ over the ranks of `count` doubles at buf (device, in place, stream s): ncclAllReduce on
 // the RCCL communicator, or the in-process group's host sum; a no-op on one rank.
 int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
@@ -478,6 +491,10 @@ int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
   }
   if (!ctx->lgroup) return 0;
   LocalGroup& G = *ctx->lgroup;
+  {
+    std::lock_guard<std::mutex> lk(G.mu);
+    if (G.aborted) return fail(ctx, -3, "local all-reduce: another rank left the group");
+  }
   std::vector<double> mine(count);
   HIPCHK(hipMemcpyAsync(mine.data(), buf, count * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -501,8 +518,12 @@ int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
       G.arrived = 0;
       ++G.gen;
       G.cv.notify_all();
-    } else if (!G.cv.wait_for(lk, std::chrono::seconds(300), [&] { return G.gen != my; })) {
+    } else if (!G.cv.wait_for(lk, std::chrono::seconds(60),
+                              [&] { return G.gen != my || G.aborted; })) {
       return fail(ctx, -3, "local all-reduce: timed out waiting for the other ranks");
+    } else if (G.gen == my) {
+      --G.arrived;
+      return fail(ctx, -3, "local all-reduce: another rank left the group");
     }
     out = G.sum;
     bad = G.last_mismatch;
@@ -908,6 +929,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  leave_local_group(ctx);
   DBuf* all[] = {&ctx->info, &ctx->small, &ctx->X, &ctx->y, &ctx->Xt, &ctx->yt, &ctx->A,
                  &ctx->Linv, &ctx->W, &ctx->logdiag, &ctx->beta, &ctx->alpha, &ctx->dinv,
                  &ctx->slab, &ctx->mu_loo, &ctx->var_loo, &ctx->Ksf, &ctx->s1, &ctx->s2,
@@ -2267,8 +2289,9 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   {
     Prof pr(ctx, "fitc_pred_finalize", 0, 8.0 * ntp * mp);
     HIPCHK(launch_gemv_full(ctx->Ksm.d(), mp, ctx->c.d(), ctx->fmu.d(), (int)ntp, (int)mp, s));
-    HIPCHK(launch_fitc_pred_finalize(ctx->qm.d(), ctx->qb.d(), (int)nt, th.sn2 + th.sf2,
-                                     ctx->fvar.d(), s));
+    if (nt > 0)  // a rank may hold no test rows; its zero score partials still join the sum
+      HIPCHK(launch_fitc_pred_finalize(ctx->qm.d(), ctx->qb.d(), (int)nt, th.sn2 + th.sf2,
+                                       ctx->fvar.d(), s));
     if (nt > 0)
       HIPCHK(launch_score_sums(ctx->fmu.d(), ctx->fvar.d(), ctx->fyt.d(), (int)nt, ctx->f_ytr_mean,
                                ctx->f_ytr_var, sums, s));
@@ -2301,7 +2324,7 @@ int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]) {
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
-  ctx->lgroup.reset();
+  leave_local_group(ctx);
   ncclUniqueId id;
   memcpy(&id, uid, 128);
   NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, id, rank));
@@ -2317,6 +2340,7 @@ int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
     ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  leave_local_group(ctx);
   std::lock_guard<std::mutex> lk(g_groups_mu);
   std::shared_ptr<LocalGroup> G = g_groups[group].lock();
   if (!G) {
@@ -2336,7 +2360,7 @@ int gps_comm_destroy(gps_ctx* ctx) {
   if (int rc = bind(ctx)) return rc;
   if (ctx->comm) NCCLCHK(ncclCommDestroy(ctx->comm));
   ctx->comm = nullptr;
-  ctx->lgroup.reset();
+  leave_local_group(ctx);
   ctx->nranks = 1;
   ctx->rank = 0;
   return 0;

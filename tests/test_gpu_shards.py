@@ -77,27 +77,53 @@ def _whole(X, y, Xt, yt, Z, th, with_grad, gpu_ctx):
     return _run(gp, th, with_grad)
 
 
-def _compare(parts, ref, tol_obj, tol_vec, tol_grad):
-    for p in parts:  # global quantities: identical on every rank
+def _diffs(parts, ref):
+    """relative differences of every global quantity (max over ranks) and of the
+    concatenated row-sharded vectors"""
+    out = {}
+    for p in parts:
         for k in OBJS:
-            assert abs(p["obj"][k] - ref["obj"][k]) <= tol_obj * max(1.0, abs(ref["obj"][k])), k
+            out[k] = max(out.get(k, 0.0), abs(p["obj"][k] - ref["obj"][k]) / max(1.0, abs(ref["obj"][k])))
         for k, v in ref["sc"].items():
-            assert abs(p["sc"][k] - v) <= tol_obj * max(1.0, abs(v)), k
+            out[k] = max(out.get(k, 0.0), abs(p["sc"][k] - v) / max(1.0, abs(v)))
         for k in ref:
             if k.startswith("g"):
-                assert nrel(p[k], ref[k]) <= tol_grad, k
-    for k in ("mu_loo", "var_loo", "mu", "var"):  # row-sharded vectors, concatenated
-        assert nrel(np.concatenate([p[k] for p in parts]), ref[k]) <= tol_vec, k
+                out[k] = max(out.get(k, 0.0), nrel(p[k], ref[k]))
+    for k in ("mu_loo", "var_loo", "mu", "var"):
+        out[k] = nrel(np.concatenate([p[k] for p in parts]), ref[k])
+    return out
+
+
+def _floor(X, y, Xt, yt, Z, th, with_grad, gpu_ctx, ref):
+    """This problem's conditioning floor, measured: the unsharded fit at inputs perturbed
+    by 1e-15 (relative; two draws) moves every output by this much.  A shard split only
+    reorders sums, so it must stay within a small multiple of it."""
+    fl = {}
+    for seed in (1, 2):
+        rng = np.random.default_rng(seed)
+        Xp = X * (1 + 1e-15 * rng.standard_normal(X.shape))
+        Zp = Z * (1 + 1e-15 * rng.standard_normal(Z.shape))
+        for k, v in _diffs([_whole(Xp, y, Xt, yt, Zp, th, with_grad, gpu_ctx)], ref).items():
+            fl[k] = max(fl.get(k, 0.0), v)
+    return fl
+
+
+def _compare(parts, ref, floor, factor=30.0, abs_min=1e-13):
+    d = _diffs(parts, ref)
+    for k, v in sorted(d.items()):
+        print(f"{k:16s} sharded {v:.2e}  floor {floor[k]:.2e}")
+    bad = {k: (v, floor[k]) for k, v in d.items() if v > factor * floor[k] + abs_min}
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("P", [2, 3])
 def test_fitc_shards_match_unsharded(gpu_ctx, P):
     """n = 6001 (ragged shards), m = 300, d = 8: forward, predict, scores and the θ / Z
-    gradients of all three objectives."""
+    gradients of all three objectives, each within 30× its measured conditioning floor."""
     X, y, Xt, yt, Z, th = _case(6001, 1501, 300, 8, 41)
     ref = _whole(X, y, Xt, yt, Z, th, True, gpu_ctx)
     parts = _sharded(P, X, y, Xt, yt, Z, th, True)
-    _compare(parts, ref, 1e-12, 1e-11, 1e-10)
+    _compare(parts, ref, _floor(X, y, Xt, yt, Z, th, True, gpu_ctx, ref))
 
 
 def test_fitc_shards_golden(gpu_ctx):
@@ -118,7 +144,7 @@ def test_fitc_shards_empty_test_shard(gpu_ctx):
     X, y, Xt, yt, Z, th = _case(900, 2, 60, 4, 43)
     ref = _whole(X, y, Xt, yt, Z, th, False, gpu_ctx)
     parts = _sharded(3, X, y, Xt, yt, Z, th, False)
-    _compare(parts, ref, 1e-12, 1e-11, 1e-10)
+    _compare(parts, ref, _floor(X, y, Xt, yt, Z, th, False, gpu_ctx, ref))
 
 
 def test_block_loo_refuses_shards(gpu_ctx):
