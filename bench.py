@@ -15,9 +15,12 @@ fit (Gram + Cholesky + L⁻¹ + α + diag(A⁻¹) → NLML, LOO-CRPS, LOO-LogS) 
   predictive TRMM) — algorithmic flops / summed kernel time from hipEvents
   recorded on the library's stream over the timed region; ``roofline_gram`` the
   HBM-bound Gram kernel.
-* ``cpu_baseline``: the oracle's ref-mirror restatement of the reference op
-  sequence (oracle/gp_oracle.py, numpy/LAPACK, all threads) timed on one full C3
-  unit (~1 min on the box's 16 host threads); rank 0 at N = 1 only.
+* ``cpu_baseline``: the torch-CPU fp64 ref-mirror of the reference op sequence
+  (oracle/ref_torch.py, all host threads) timed on one full C3 unit; rank 0 at N = 1
+  only.  ``parity``: every output of the GPU unit against that run's outputs (same
+  inputs).  ``c1``: BASELINE.json configs[0] (SIMPLE-DATA n = 500, d = 1, rbf) on the
+  GPU and on the host.  ``fitc.C4.cpu_baseline``: dense FITC ref-mirror (n³-extrapolated)
+  and the Woodbury numpy restatement.
 
 Inputs are synthetic (SURVEY.md §8d generator) and resident in HBM before the
 timed region.  Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -185,25 +188,142 @@ def roofline_gram(prof, steps=1, traffic=None, tags=("gram_kff", "gram_ksf")):
             "bytes_per_launch": b / max(1, sum(1 for t in tags if t in prof))}
 
 
-def cpu_baseline():
-    """ref-mirror oracle (the reference op sequence) on the full C3 workload, one unit.
-
-    Timed directly rather than extrapolated: C2 × 64 (O(n³)) overstated the C3 time 2.6×
-    on the MI355X box host (151 s vs 57.5 s measured, profiles/r1h_cpu_c3_direct.json) —
-    host BLAS runs much closer to peak at n = 20 000 than at 5 000."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+def _oracle():
+    for sub in ("oracle",):
+        p = os.path.join(ROOT, sub)
+        if p not in sys.path:
+            sys.path.insert(0, p)
     import gp_oracle as O
-    c = CONFIGS["C3"]
+    import ref_torch as RT
+    return O, RT
+
+
+def _torch_threads():
+    """All host threads the box gives this process (OMP_NUM_THREADS is set there)."""
+    import torch
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    return cores
+
+
+def cpu_baseline(config="C3"):
+    """The reference op sequence in the reference's own framework — torch-CPU fp64 ref-mirror
+    (oracle/ref_torch.py: upper potrf + 2 LU solves per chol_solve, LOO diag by
+    chol_solve(I, A), full n*×n* covariance; KF:239-245, 329-334, 365-391) — timed on ONE
+    full C3 unit on the box's host threads (BASELINE.md:48-57).  Also returns its outputs,
+    which the parity record compares with the GPU unit."""
+    _, RT = _oracle()
+    cores = _torch_threads()
+    c = CONFIGS[config]
     X, y, Xt, yt, _, th = synth(c["n"], c["d"], c["nt"], c["seed"])
     t0 = time.perf_counter()
-    O.ref_full(X, y, Xt, yt, *th)
+    ref = RT.ref_full(X, y, Xt, yt, *th)
     t = time.perf_counter() - t0
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": 1.0 / t, "unit": "fit+predict+score units/s (C3)",
-            "cores": cores, "kind": "port",
-            "sample": f"oracle ref_full (reference op sequence: upper potrf + 2 LU solves per "
-                      f"chol_solve, full n*×n* cov) on the full C3 workload n={c['n']} "
-                      f"d={c['d']} n*={c['nt']}, one unit: {t:.1f} s"}
+    info = RT.host_info()
+    return {"value": 1.0 / t, "unit": f"fit+predict+score units/s ({config})",
+            "cores": cores, "kind": "port", "host": info,
+            "sample": f"torch-CPU fp64 ref-mirror of the reference op sequence on the full C3 "
+                      f"workload {config} n={c['n']} d={c['d']} n*={c['nt']}, one unit: {t:.1f} s "
+                      f"({info['cpu_model']}, {cores} threads, BLAS {info['blas']})"}, ref
+
+
+PARITY_VECS = ("loo_mu", "loo_var", "pred_mu", "pred_var")
+PARITY_SCAL = ("nlml", "loo_crps", "loo_logs", "logdet", "quad", "test_crps", "test_logs",
+               "test_msll", "test_smse", "test_mse", "test_cover")
+
+
+def parity(got, ref):
+    """normwise relative error of every output of the unit against the oracle run on the
+    same inputs: max|a − b| / max|b| for vectors, |a − b| / max(1, |b|) for scalars."""
+    out = {}
+    for k in PARITY_VECS:
+        a, b = np.asarray(got[k], np.float64), np.asarray(ref[k], np.float64)
+        out[k] = float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+    for k in PARITY_SCAL:
+        out[k] = abs(float(got[k]) - float(ref[k])) / max(1.0, abs(float(ref[k])))
+    out["max"] = max(out.values())
+    return out
+
+
+def gpu_unit_outputs(gp, th, rbf=False):
+    r = gp.fit(theta=th, rbf=rbf)
+    mu, var, sc = gp.predict(with_scores=True)
+    out = dict(r.objectives)
+    out.update(loo_mu=r.mu_loo, loo_var=r.var_loo, pred_mu=mu, pred_var=var)
+    out.update(sc)
+    return out
+
+
+def synth_c1(n=500, nt=500, seed=1):
+    """C1: the SIMPLE-DATA generator (SD:158-181) at n = 500 — x = 2·N(0, 1), y ~ MVN(0,
+    rbf(x, x; log k² = 0, log ℓ² = 0) + 0.3²·I), split train / test — drawn with numpy (the
+    reference draws with torch.manual_seed(100 j)); the fit uses the rbf kernel at the
+    generating hyper-parameters (log sf² = 0, b = log ℓ² = 0, log σ² = log 0.09)."""
+    rng = np.random.default_rng(seed)
+    x = 2.0 * rng.standard_normal(n + nt)
+    K = np.exp(-0.5 * (x[:, None] - x[None, :]) ** 2) + 0.09 * np.eye(n + nt)
+    yy = np.linalg.cholesky(K) @ rng.standard_normal(n + nt)
+    th = (0.0, 0.0, np.log(0.09))
+    return x[:n, None], yy[:n], x[n:, None], yy[n:], th
+
+
+def c1_leg(ctx, steps):
+    """BASELINE.json configs[0]: the SIMPLE-DATA full GP at n = 500, d = 1, rbf — the GPU
+    unit, the torch-CPU ref-mirror of the same unit (median of 5), and their parity."""
+    import gpscore
+    O, RT = _oracle()
+    X, y, Xt, yt, th = synth_c1()
+    gp = gpscore.GP(ctx=ctx)
+    gp.set_data(X, y)
+    gp.set_test(Xt, yt)
+    got = gpu_unit_outputs(gp, th, rbf=True)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gp.fit(theta=th, rbf=True, return_loo=False)
+        gp.predict(with_scores=True)
+    ctx.synchronize()
+    ms_gpu = 1e3 * (time.perf_counter() - t0) / steps
+    cores = _torch_threads()
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ref = RT.ref_full(X, y, Xt, yt, *th, kind="rbf")
+        ts.append(time.perf_counter() - t0)
+    return {"config": "C1 SIMPLE-DATA full GP n=500 d=1 rbf, n*=500 (SD:158-213 generator)",
+            "ms_per_step": ms_gpu, "cpu_ref_ms": 1e3 * float(np.median(ts)), "cpu_cores": cores,
+            "speedup_vs_cpu": float(np.median(ts)) * 1e3 / ms_gpu, "parity": parity(got, ref),
+            "note": "host round trips included: at n = 500 the unit is launch/PCIe bound"}
+
+
+def fitc_cpu_baseline():
+    """FITC at C4 on the host (BASELINE.md:56-57): the dense torch ref-mirror (K20:222-234,
+    329-340, 434-447, 270-296: n×n big_Q, chol_solve = potrf + 2 LU) timed at
+    (n, n*) = (5000, 1250) and (10000, 2500) with C4's m = 2000 and d = 8, extrapolated
+    as n³ (n* ∝ n) to (40000, 10000) — a 12.8 GB n×n matrix per copy, ~20 min — and the
+    O(n·m²) Woodbury numpy restatement timed directly at C4."""
+    O, RT = _oracle()
+    cores = _torch_threads()
+    c = CONFIGS["C4"]
+    times = {}
+    for n in (5000, 10000):
+        X, y, Xt, yt, Z, th = synth(n, c["d"], n // 4, c["seed"], c["m"])
+        t0 = time.perf_counter()
+        RT.ref_fitc(X, y, Xt, yt, Z, *th)
+        times[n] = time.perf_counter() - t0
+    extrap = times[10000] * (c["n"] / 10000) ** 3
+    X, y, Xt, yt, Z, th = synth(c["n"], c["d"], c["nt"], c["seed"], c["m"])
+    t0 = time.perf_counter()
+    O.fast_fitc(X, y, Xt, yt, Z, *th)
+    t_fast = time.perf_counter() - t0
+    return {"value": 1.0 / extrap, "unit": "fit+predict+score units/s (C4)", "cores": cores,
+            "kind": "port",
+            "sample": f"dense torch-CPU ref-mirror FITC at n=5000 / 10000 (n*=n/4, m=2000, d=8): "
+                      f"{times[5000]:.1f} / {times[10000]:.1f} s, n^3-extrapolated to C4: "
+                      f"{extrap:.0f} s per unit",
+            "woodbury_numpy_s": t_fast,
+            "woodbury_note": "O(n·m²) numpy/LAPACK restatement (the GPU's algorithm) on the full C4 "
+                             "unit — not the reference algorithm"}
 
 
 def main():
@@ -394,9 +514,17 @@ def main():
         res["fitc"] = fitc
 
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline()
+        cb, ref = cpu_baseline(args.config)
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
+        got = gpu_unit_outputs(gp, th)
+        res["parity"] = {"vs": f"torch-CPU ref-mirror (reference op sequence) on the same "
+                               f"{args.config} inputs",
+                         "metric": "normwise relative error (vectors: max|a-b|/max|b|; scalars: "
+                                   "|a-b|/max(1,|b|))", **parity(got, ref)}
+        res["c1"] = c1_leg(ctx, args.steps)
+        if "fitc" in res and "C4" in res["fitc"]:
+            res["fitc"]["C4"]["cpu_baseline"] = fitc_cpu_baseline()
     if args.rehearse:
         res["rehearsal"] = "all ranks on device 0, no RCCL: not a measurement"
     if rank == 0:

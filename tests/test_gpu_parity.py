@@ -133,22 +133,14 @@ def test_c2_config_vs_oracle(gp):
 
 def test_c4_config_vs_oracle(gp):
     """C4 exactly as bench.py builds it (FITC n = 40 000, m = 2000, n* = 10 000, d = 8)
-    against the O(n·m²) Woodbury oracle (~15 s of host BLAS).
-
-    Tolerances are this problem's conditioning floor, not the kernel's: cond(K̃mm) ≈ 4e5
-    here, and perturbing X and Z by 1e-15 (relative) moves the ORACLE's own outputs by
-    loo_mu / pred_mu 3.6e-7, loo_var / pred_var 1.4e-9, nlml 2.3e-8, quad 1.9e-8,
-    loo_logs 1.7e-8 (measured in this container).  The bounds below are ~5x that floor."""
+    against the O(n·m²) Woodbury oracle (~15 s of host BLAS).  cond(K̃mm) ≈ 4e5 here, so
+    the floor is far above the full GP's; it is measured in the test (_measured_floor),
+    not assumed."""
     X, y, Xt, yt, Z, th = _bench_inputs("C4")
-    out = O.fast_fitc(X, y, Xt, yt, Z, *th)
-    got = _gpu_case(gp, {"X": X, "y": y, "Xt": Xt, "yt": yt, "Z": Z, "log_sf2": th[0],
-                         "log_ell": th[1], "log_sn2": th[2]}, "fitc", fitc=True)
-    vec_tol = {"loo_mu": 2e-6, "pred_mu": 2e-6, "loo_var": 1e-8, "pred_var": 1e-8}
-    for k, tol in vec_tol.items():
-        assert nrel(got[k], out[k]) <= tol, (k, nrel(got[k], out[k]))
-    for k in SCAL_KEYS:
-        ref = float(out[k])
-        assert abs(got[k] - ref) <= 2e-7 * max(1.0, abs(ref)), (k, got[k], ref)
+    got = _unit(gp, X, y, Xt, yt, th, Z=Z)
+    floor = _measured_floor(gp, got, X, y, Xt, yt, th, Z=Z)
+    ref = O.fast_fitc(X, y, Xt, yt, Z, *th)
+    _check_vs_oracle(got, ref, floor, len(yt))
 
 
 def test_c3_config_properties(gp):
@@ -183,6 +175,88 @@ def test_c3_config_properties(gp):
     assert abs(o["quad"] - y @ alpha) < 1e-8 * abs(o["quad"])
     assert abs(o["nlml"] - (0.5 * n * np.log(2 * np.pi) + 0.5 * o["logdet"] + 0.5 * o["quad"])) \
         < 1e-9 * abs(o["nlml"])
+
+
+# ---------------------------------------------------------------------------------------
+# The BASELINE.json configs exactly as bench.py builds them, against the oracle, with every
+# tolerance taken from this problem's conditioning floor MEASURED in the test: the unit is
+# re-run on the GPU at inputs perturbed by 1e-15 (relative, two draws), and the GPU-vs-oracle
+# difference of each output must stay within 30× the movement that perturbation causes (two
+# correct fp64 implementations that round differently differ by about that much).
+UNIT_VECS = ("loo_mu", "loo_var", "pred_mu", "pred_var")
+UNIT_SCAL = ("nlml", "loo_crps", "loo_logs", "logdet", "quad", "test_crps", "test_logs",
+             "test_msll", "test_smse", "test_mse", "test_cover")
+
+
+def _unit(gp, X, y, Xt, yt, th, Z=None, rbf=False):
+    if Z is None:
+        gp.set_data(X, y)
+    else:
+        gp.set_data(X, y, kind="fitc", Z=Z)
+    gp.set_test(Xt, yt)
+    r = gp.fit(theta=th, rbf=rbf)
+    mu, var, sc = gp.predict(with_scores=True)
+    out = dict(r.objectives)
+    out.update(loo_mu=r.mu_loo, loo_var=r.var_loo, pred_mu=mu, pred_var=var, **sc)
+    return out
+
+
+def _rel(a, b):
+    out = {k: nrel(a[k], b[k]) for k in UNIT_VECS}
+    out.update({k: abs(float(a[k]) - float(b[k])) / max(1.0, abs(float(b[k]))) for k in UNIT_SCAL})
+    return out
+
+
+def _measured_floor(gp, base, X, y, Xt, yt, th, Z=None, rbf=False):
+    fl = {}
+    for seed in (1, 2):
+        rng = np.random.default_rng(seed)
+        pert = [a * (1 + 1e-15 * rng.standard_normal(a.shape)) if a is not None else None
+                for a in (X, Xt, Z)]
+        for k, v in _rel(_unit(gp, pert[0], y, pert[1], yt, th, pert[2], rbf), base).items():
+            fl[k] = max(fl.get(k, 0.0), v)
+    return fl
+
+
+def _check_vs_oracle(got, ref, floor, nt, factor=30.0):
+    d = _rel(got, ref)
+    for k in UNIT_VECS + UNIT_SCAL:
+        print(f"{k:10s} gpu-vs-oracle {d[k]:.2e}  floor {floor[k]:.2e}")
+    # the ±2σ coverage is a count: a point on the band's edge may flip
+    slack = {k: (2.0 / nt if k == "test_cover" else 1e-14) for k in d}
+    bad = {k: (d[k], floor[k]) for k in d if d[k] > factor * floor[k] + slack[k]}
+    assert not bad, bad
+
+
+def test_c1_config_vs_torch_ref(gp):
+    """C1 (BASELINE.json configs[0], SIMPLE-DATA n = 500, d = 1, rbf; bench.synth_c1) against
+    the torch-CPU ref-mirror of the reference op sequence (oracle/ref_torch.py)."""
+    import bench
+    import ref_torch as RT
+    X, y, Xt, yt, th = bench.synth_c1()
+    got = _unit(gp, X, y, Xt, yt, th, rbf=True)
+    ref = RT.ref_full(X, y, Xt, yt, *th, kind="rbf")
+    _check_vs_oracle(got, ref, _measured_floor(gp, got, X, y, Xt, yt, th, rbf=True), len(yt))
+
+
+def test_c3_config_vs_oracle(gp):
+    """C3, the headline (n = 20 000, n* = 5000, d = 8), against the fast oracle on the same
+    inputs (~20-40 s of host LAPACK; KF:239-245, 329-334, 365-391)."""
+    X, y, Xt, yt, _, th = _bench_inputs("C3")
+    got = _unit(gp, X, y, Xt, yt, th)
+    floor = _measured_floor(gp, got, X, y, Xt, yt, th)
+    ref = O.fast_full(X, y, Xt, yt, *th)
+    _check_vs_oracle(got, ref, floor, len(yt))
+
+
+def test_c5_config_vs_oracle(gp):
+    """C5 at N = 1 (FITC n = 200 000, m = 4000, d = 16, n* = 10 000) against the O(n·m²)
+    Woodbury oracle (~30-60 s of host BLAS; K20:222-234, 329-340, 270-296)."""
+    X, y, Xt, yt, Z, th = _bench_inputs("C5")
+    got = _unit(gp, X, y, Xt, yt, th, Z=Z)
+    floor = _measured_floor(gp, got, X, y, Xt, yt, th, Z=Z)
+    ref = O.fast_fitc(X, y, Xt, yt, Z, *th)
+    _check_vs_oracle(got, ref, floor, len(yt))
 
 
 def test_stream_schedules_agree(gp, gpu_ctx):

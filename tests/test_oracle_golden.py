@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 import gp_oracle as O
+import ref_torch as RT
 from conftest import golden_names, load_golden, nrel, theta_of
 
 VEC_KEYS = ("loo_mu", "loo_var", "pred_mu", "pred_var")
@@ -23,11 +24,13 @@ def _check(out, g, tol):
 
 
 @pytest.mark.parametrize("name", FULL)
-@pytest.mark.parametrize("flavour", ["ref", "fast"])
+@pytest.mark.parametrize("flavour", ["ref", "fast", "torch"])
 def test_full_oracle_vs_golden(name, flavour):
+    """ref / fast: the numpy restatements; torch: the torch-CPU ref-mirror the bench times
+    as the CPU baseline (oracle/ref_torch.py)."""
     g = load_golden(name)
     th, kind = theta_of(g)
-    fn = O.ref_full if flavour == "ref" else O.fast_full
+    fn = {"ref": O.ref_full, "fast": O.fast_full, "torch": RT.ref_full}[flavour]
     out = fn(g["X"], g["y"], g["Xt"], g["yt"], *th, kind="rbf" if kind == "rbf" else "ARD")
     _check(out, g, 1e-9)
 
@@ -49,12 +52,14 @@ def test_oracle_gradients_vs_autograd(name, obj):
 
 
 @pytest.mark.parametrize("name", FITC)
-@pytest.mark.parametrize("flavour", ["ref", "fast", "shard3"])
+@pytest.mark.parametrize("flavour", ["ref", "fast", "shard3", "torch"])
 def test_fitc_oracle_vs_golden(name, flavour):
     g = load_golden(name)
     th, _ = theta_of(g)
     if flavour == "ref":
         out = O.ref_fitc(g["X"], g["y"], g["Xt"], g["yt"], g["Z"], *th)
+    elif flavour == "torch":
+        out = RT.ref_fitc(g["X"], g["y"], g["Xt"], g["yt"], g["Z"], *th)
     else:
         out = O.fast_fitc(g["X"], g["y"], g["Xt"], g["yt"], g["Z"], *th,
                           shards=3 if flavour == "shard3" else 1)
