@@ -333,7 +333,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   hipStream_t s = ctx->stream;
   if (nb == 1) {
     Prof pr(ctx, "potrf_diag128", 2.0 * 128 * 128 * 128 / 3.0, 0);
-    HIPCHK(launch_potrf_diag(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, s));
+    HIPCHK(launch_potrf_leaf(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, s));
     return 0;
   }
   const int n1b = nb / 2, n2b = nb - n1b;

@@ -137,13 +137,14 @@ hipError_t launch_gram(const GramParams& p, hipStream_t s);
 // C = alpha * op(A) op(B) + beta * C with the epilogue selected by `epi`
 hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& p, hipStream_t s);
 
-// diagonal 128×128 block: in-LDS Cholesky + triangular inverse.
-// Reads the lower triangle of A (lda), writes L⁻¹ (lower, upper zeroed) into
-// Linv (ldl) and log(L_ii) into logdiag[0..127]; sets *info (atomicMin) to the
-// 1-based global index of the first non-positive pivot.
-hipError_t launch_potrf_diag(const double* A, int64_t lda, double* Linv, int64_t ldl,
+// leaf of the recursive Cholesky: the diagonal 128×128 block, Cholesky + triangular inverse
+// in one workgroup (kernels_potrf.hip).  Reads the lower triangle of A (lda), writes L⁻¹
+// (lower, zeros above the diagonal) into Linv (ldl), L into Lout (optional), log(L_ii) into
+// logdiag[0..127]; sets *info (atomicMin) to the 1-based global index of the first
+// non-positive pivot.
+hipError_t launch_potrf_leaf(const double* A, int64_t lda, double* Linv, int64_t ldl,
                              double* Lout, int64_t ldlo, double* logdiag, int* info,
-                             int base_index, int n_real_in_block, hipStream_t s);
+                             int base, int n_real_in_block, hipStream_t s);
 
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)
 hipError_t launch_gemv_lower(const double* L, int64_t ldl, const double* x, double* y,

@@ -323,7 +323,7 @@ __global__ __launch_bounds__(64 * V3_WAVES) void potrf_diag_v3_kernel(
   }
 }
 
-hipError_t launch_potrf_diag(const double* A, int64_t lda, double* Linv, int64_t ldl, double* Lout,
+hipError_t launch_potrf_leaf(const double* A, int64_t lda, double* Linv, int64_t ldl, double* Lout,
                              int64_t ldlo, double* logdiag, int* info, int base, int nreal,
                              hipStream_t s) {
   if ((lda & 1) || (ldl & 1) || (Lout && (ldlo & 1))) return hipErrorInvalidValue;

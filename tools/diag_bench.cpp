@@ -1,13 +1,17 @@
-// Timing + correctness of the 128×128 diagonal-block kernel (potrf + inverse).
-// tools/run_diag_bench.sh builds it for the production kernel (v3) and for -DGPS_DIAG_V1.
+// Timing + correctness of the 128×128 leaf kernel (potrf + inverse): the library's kernel
+// (csrc/kernels_potrf.hip) against the MFMA-tiled experiment (tools/leaf_mfma.hip), same box.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <string.h>
 #include <algorithm>
 #include <vector>
 #include "kernels_potrf.hip"
+#include "leaf_mfma.hip"
 using namespace gps;
-int main() {
+typedef hipError_t (*LeafFn)(const double*, int64_t, double*, int64_t, double*, int64_t, double*,
+                             int*, int, int, hipStream_t);
+static int run(const char* name, LeafFn launch_potrf_diag) {
   const int n = 128;
   std::vector<double> h(n * n);
   for (int i = 0; i < n; ++i)
@@ -64,27 +68,21 @@ int main() {
   hipEventRecord(e1); hipEventSynchronize(e1);
   hipEventElapsedTime(&ms, e0, e1);
   printf("%.2f us per diag block (with Lout)\n", 1e3 * ms / reps);
-#ifdef GPS_V3_STAMPS
-  {
-    std::vector<unsigned long long> st(32 * 8);
-    hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(gps_stamps3), st.size() * 8);
-    double sum[7] = {0};
-    const char* nm[7] = {"update", "pivot", "panelL+CB", "P+PT", "DI/DG", "barrier", "->next"};
-    for (int jb = 0; jb < 32; ++jb) {
-      double d[7];
-      for (int k = 0; k < 6; ++k) d[k] = (double)(st[jb * 8 + k + 1] - st[jb * 8 + k]);
-      d[6] = jb < 31 ? (double)(st[(jb + 1) * 8] - st[jb * 8 + 6]) : 0.0;
-      for (int k = 0; k < 7; ++k) sum[k] += d[k];
-      if (jb < 3 || jb == 15 || jb == 30)
-        printf("jb=%2d upd %5.0f piv %5.0f L %5.0f P %5.0f DI %5.0f bar %5.0f next %5.0f\n", jb,
-               d[0], d[1], d[2], d[3], d[4], d[5], d[6]);
-    }
-    printf("sums:");
-    for (int k = 0; k < 7; ++k) printf(" %s %.0f", nm[k], sum[k]);
-    printf("\n");
-  }
-#endif
-  const bool ok = eL < 1e-12 && eX < 1e-12 && eD < 1e-13 && ginfo == 0x7f7f7f7f;
-  printf("%s\n", ok ? "PASS" : "FAIL");
+  // non-PD pivot at row 77: info must be 78
+  h[77 * n + 77] = -1.0;
+  hipMemcpy(A, h.data(), n * n * 8, hipMemcpyHostToDevice);
+  hipMemset(info, 0x7f, 4);
+  launch_potrf_diag(A, n, Li, n, nullptr, 0, ld, info, 0, n, 0);
+  int binfo = 0;
+  hipMemcpy(&binfo, info, 4, hipMemcpyDeviceToHost);
+  printf("non-PD at 77 -> info %d\n", binfo);
+  const bool ok = eL < 1e-12 && eX < 1e-12 && eD < 1e-13 && ginfo == 0x7f7f7f7f && binfo == 78;
+  printf("%s: %s\n", name, ok ? "PASS" : "FAIL");
   return ok ? 0 : 1;
+}
+
+int main(int argc, char** argv) {
+  int rc = run("library leaf (kernels_potrf.hip)", launch_potrf_leaf);
+  if (argc < 2 || strcmp(argv[1], "lib") != 0) rc |= run("MFMA-tiled leaf (tools/leaf_mfma.hip)", launch_potrf_leaf_mfma);
+  return rc;
 }
