@@ -296,6 +296,34 @@ def c1_leg(ctx, steps):
             "note": "host round trips included: at n = 500 the unit is launch/PCIe bound"}
 
 
+def surface_leg(ctx, steps, with_cpu):
+    """contour-plot.R's four objective surfaces (CP.R:43-85) on its 50 × 50
+    (length-scale, noise s.d.) grid at n = 20 (CP.R:88-141): 2500 small full GPs, one wavefront
+    each, per call.  CPU: the oracle's numpy ref-mirror of the same grid (CP.R's op sequence)."""
+    import gpscore
+    O, _ = _oracle()
+    x, y = O.cp_data(seed=0)
+    ell, sd = np.linspace(0.01, 2.0, 50), np.linspace(0.01, 1.0, 50)
+    got = gpscore.surface(x, y, ell, sd, ctx=ctx)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gpscore.surface(x, y, ell, sd, ctx=ctx)
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    res = {"config": "CP.R grid 50 x 50 (l in [0.01, 2], noise s.d. in [0.01, 1]), n = 20, d = 1",
+           "ms_per_surface": ms, "grid_points_per_s": 2500 / (ms * 1e-3),
+           "note": "4 objectives per grid point (LOO-CRPS, in-sample CRPS, NLML, LOO-LogS); host "
+                   "round trip included"}
+    if with_cpu:
+        t0 = time.perf_counter()
+        ref = O.cp_surface(x, y, ell, sd)
+        res["cpu_ref_ms"] = 1e3 * (time.perf_counter() - t0)
+        res["parity_max_nrel"] = max(
+            float(np.max(np.abs(got[k] - ref[i])) / np.max(np.abs(ref[i])))
+            for i, k in enumerate(("loo_crps", "insample_crps", "nlml", "loo_logs")))
+    return res
+
+
 def fitc_cpu_baseline():
     """FITC at C4 on the host (BASELINE.md:56-57): the dense torch ref-mirror (K20:222-234,
     329-340, 434-447, 270-296: n×n big_Q, chol_solve = potrf + 2 LU) timed at
@@ -513,6 +541,7 @@ def main():
             ctx.call("gps_comm_destroy")
         res["fitc"] = fitc
 
+    res["surface"] = surface_leg(ctx, args.steps, rank == 0 and world == 1 and not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu:
         cb, ref = cpu_baseline(args.config)
         res["cpu_baseline"] = cb

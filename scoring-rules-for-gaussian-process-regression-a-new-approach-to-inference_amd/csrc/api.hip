@@ -2307,6 +2307,37 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   return 0;
 }
 
+// ------------------------------------------------------------- CP.R surfaces
+int gps_full_surface(gps_ctx* ctx, const double* X, const double* y, int64_t n, int d,
+                     double log_sf2, const double* ell, int64_t n_ell, const double* noise_sd,
+                     int64_t n_noise, int flags, double* out) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(X && y && ell && noise_sd && out, "NULL argument");
+  ARGCHK(n >= 1 && n <= GPS_SURFACE_MAX_N, "surface: n must be in 1..128 (one wavefront per point)");
+  ARGCHK(d >= 1 && d <= GPS_MAX_D, "bad d");
+  ARGCHK(n_ell >= 1 && n_noise >= 1 && n_ell * n_noise <= (1 << 24), "bad grid");
+  ARGCHK((flags & ~GPS_SURF_LOGS_ADD_NOISE) == 0, "unknown surface flag");
+  hipStream_t s = ctx->stream;
+  if (int rc = upload(ctx, ctx->t0, X, n, d, n)) return rc;
+  if (int rc = upload(ctx, ctx->t1, y, n, 1, n)) return rc;
+  if (int rc = upload(ctx, ctx->t2, ell, n_ell, 1, n_ell)) return rc;
+  if (int rc = upload(ctx, ctx->t3, noise_sd, n_noise, 1, n_noise)) return rc;
+  const int64_t cnt = 4 * n_ell * n_noise;
+  HIPCHK(ensure(ctx->t4, (size_t)cnt * 8));
+  SurfaceParams p;
+  p.x = ctx->t0.d(); p.y = ctx->t1.d(); p.n = (int)n; p.d = d; p.sf2 = std::exp(log_sf2);
+  p.ell = ctx->t2.d(); p.nl = (int)n_ell; p.sd = ctx->t3.d(); p.ns = (int)n_noise;
+  p.logs_add_noise = (flags & GPS_SURF_LOGS_ADD_NOISE) != 0;
+  p.out = ctx->t4.d();
+  {
+    Prof pr(ctx, "surface", 0, 0);
+    HIPCHK(launch_surface(p, s));
+  }
+  HIPCHK(hipMemcpyAsync(out, ctx->t4.p, (size_t)cnt * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
 // ---------------------------------------------------------------------- comm
 int gps_comm_unique_id(char uid[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");

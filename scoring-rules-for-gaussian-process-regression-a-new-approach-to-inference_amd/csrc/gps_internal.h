@@ -102,6 +102,19 @@ __device__ void block_sum(double (&v)[NV], double* sh) {
   __syncthreads();
 }
 
+// Gaussian CRPS and negative log density of one point (crps KF:60-68, logs KF:52-57; c is
+// the VARIANCE)
+__device__ __forceinline__ double crps_term(double m, double c, double y) {
+  const double s = sqrt(c);
+  const double z = (y - m) / s;
+  const double cdf = 0.5 * (1.0 + erf(z * 0.70710678118654752440));
+  const double pdf = 0.39894228040143267794 * exp(-z * z * 0.5);
+  return s * (z * (2.0 * cdf - 1.0) + 2.0 * pdf - 0.56418958354775628695);
+}
+__device__ __forceinline__ double logs_term(double m, double c, double y) {
+  const double e = y - m;
+  return e * e / (2.0 * c) + log(sqrt(c)) + 0.91893853320467274178;
+}
 #endif
 
 // gradient contraction: Σ_ij M_ij ∂A_ij/∂θ over the real n×n lower triangle with
@@ -132,7 +145,20 @@ struct FitcContractParams {
   int rchunk;                           // set by the launcher
 };
 
+// objective surfaces over a (length-scale, noise s.d.) grid (kernels_surface.hip, CP.R)
+#define GPS_SURFACE_MAX_N 128
+struct SurfaceParams {
+  const double* x; const double* y;  // [n][d], [n]
+  int n, d;
+  double sf2;
+  const double* ell; int nl;         // length-scales ℓ (not logs), grid columns
+  const double* sd; int ns;          // noise standard deviations s (σ² = s²), grid rows
+  int logs_add_noise;                // CP.R:81: LOO-LogS variance 1/d + s²
+  double* out;                       // [4][ns][nl]: LOO-CRPS, in-sample CRPS, NLML, LOO-LogS
+};
+
 // ------------------------------------------------------------------ launchers
+hipError_t launch_surface(const SurfaceParams& p, hipStream_t s);
 hipError_t launch_gram(const GramParams& p, hipStream_t s);
 // C = alpha * op(A) op(B) + beta * C with the epilogue selected by `epi`
 hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& p, hipStream_t s);

@@ -9,18 +9,6 @@
 
 namespace gps {
 
-__device__ __forceinline__ double crps_term(double m, double c, double y) {
-  const double s = sqrt(c);
-  const double z = (y - m) / s;
-  const double cdf = 0.5 * (1.0 + erf(z * 0.70710678118654752440));
-  const double pdf = 0.39894228040143267794 * exp(-z * z * 0.5);
-  return s * (z * (2.0 * cdf - 1.0) + 2.0 * pdf - 0.56418958354775628695);
-}
-__device__ __forceinline__ double logs_term(double m, double c, double y) {
-  const double e = y - m;
-  return e * e / (2.0 * c) + log(sqrt(c)) + 0.91893853320467274178;
-}
-
 // ------------------------------------------------------------------ GEMV rows
 // one wave per row, 16-byte loads; tile-lower: k < (i/128 + 1)*128
 __global__ __launch_bounds__(256) void gemv_rows_kernel(const double* __restrict__ M, int64_t ldm,

@@ -10,6 +10,6 @@ Drop-in layers:
 """
 from ._lib import (Context, GpsError, NotPositiveDefinite, default_context, load,  # noqa: F401
                    OBJ_NAMES, SCORE_NAMES)
-from .gp import GP, FitResult, fit, pack_theta, score  # noqa: F401
+from .gp import GP, FitResult, fit, pack_theta, score, surface  # noqa: F401
 
 __version__ = "0.1.0"

@@ -19,6 +19,8 @@ GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
+SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
+GPS_SURF_LOGS_ADD_NOISE = 1
 SCORE_NAMES = ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse", "test_cover")
 
 _c_int, _c_i64, _c_dbl, _c_vp, _c_cp = (ctypes.c_int, ctypes.c_int64, ctypes.c_double,
@@ -61,6 +63,8 @@ SIGNATURES = {
     "gps_fitc_blockloo": (_c_int, [_c_vp, _P, _c_int, _c_int, _c_int, _P, _P, _P, _P]),
     "gps_energy_score": (_c_int, [_c_vp, _P, _P, _c_i64, _P, _c_int, _c_dbl, _P, _P]),
     "gps_fitc_predict": (_c_int, [_c_vp, _P, _P, _P]),
+    "gps_full_surface": (_c_int, [_c_vp, _P, _P, _c_i64, _c_int, _c_dbl, _P, _c_i64, _P, _c_i64,
+                                  _c_int, _P]),
     "gps_comm_unique_id": (_c_int, [_c_cp]),
     "gps_comm_init": (_c_int, [_c_vp, _c_int, _c_int, _c_cp]),
     "gps_comm_init_local": (_c_int, [_c_vp, _c_int, _c_int, ctypes.c_longlong]),

@@ -19,7 +19,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import GPS_ARD, GPS_RBF, OBJ_NAMES, SCORE_NAMES, f64, ptr
+from ._lib import (GPS_ARD, GPS_RBF, GPS_SURF_LOGS_ADD_NOISE, OBJ_NAMES, SCORE_NAMES,
+                   SURFACE_NAMES, f64, ptr)
 
 BLOCK_OBJS = ["dss", "kc", "es"]  # GPS_BLOCK_DSS, GPS_BLOCK_KC, GPS_BLOCK_ES
 
@@ -297,3 +298,28 @@ def score(mu, var, y_test, y_train, ctx=None):
 
 def fit(X, y, theta, kind="full", Z=None, rbf=False, ctx=None):
     return GP(ctx).fit(X, y, theta, kind=kind, Z=Z, rbf=rbf)
+
+
+def surface(X, y, ell_grid, noise_sd_grid, log_sf2=0.0, logs_add_noise=True, ctx=None):
+    """The objective surfaces of contour-plot.R (CP.R:43-85) over a length-scale × noise grid,
+    one small full GP per grid point on the device (n <= 128).
+
+    ``ell_grid`` holds length-scales ℓ (not logs; CP.R's ``l``), ``noise_sd_grid`` noise
+    standard deviations s entering as s² (CP.R's ``j``); the kernel is
+    exp(log_sf2)·exp(−½‖x − x'‖²/ℓ²) (CP.R:15-23 with k² = exp(log_sf2)).  Returns a dict of
+    (len(noise_sd_grid), len(ell_grid)) arrays — rows noise, columns length-scale, as R's
+    ``matrix(…, nrow = 50)`` (CP.R:113-141): "loo_crps" (cal_m_crps CP.R:43-53),
+    "insample_crps" (wrong_cal_m_crps CP.R:55-64), "nlml" (cal_NLML CP.R:68-73), "loo_logs"
+    (cal_m_logs CP.R:75-85; its LOO variance carries + s² as CP.R:81 writes it unless
+    ``logs_add_noise`` is False)."""
+    ctx = ctx or _lib.default_context()
+    X = f64(X, 2)
+    y = f64(y).ravel()
+    if X.shape[0] != y.size:
+        raise ValueError("X and y disagree on n")
+    ell = f64(ell_grid).ravel()
+    sd = f64(noise_sd_grid).ravel()
+    out = np.empty((4, sd.size, ell.size))
+    ctx.call("gps_full_surface", ptr(X), ptr(y), y.size, X.shape[1], float(log_sf2), ptr(ell),
+             ell.size, ptr(sd), sd.size, GPS_SURF_LOGS_ADD_NOISE if logs_add_noise else 0, ptr(out))
+    return dict(zip(SURFACE_NAMES, out))

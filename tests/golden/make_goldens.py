@@ -371,6 +371,34 @@ def es_case(ns, X, y, log_sf2, log_ell, log_sn2, num_sim, seed):
             "draws_es": draws, "num_sim": num_sim}
 
 
+def surface_case(ns, x, y, ell_grid, sd_grid):
+    """contour-plot.R's four objectives (CP.R:43-85) on a grid, composed from the Python
+    reference defs with CP.R's parameterisation: the reference rbf (SD:8-21, b = log ℓ², so
+    b = 2 log l for CP.R's direct l; a = log k² = 0), chol_solve (KF:25-29), crps (KF:60-68),
+    logs (KF:52-57).  R itself is absent, so the R side is unpinned; this pins the algebra."""
+    X, Y = T(x).view(len(x), -1), T(y).view(-1, 1)
+    n = Y.shape[0]
+    out = np.empty((4, len(sd_grid), len(ell_grid)))
+    with torch.no_grad():
+        for i, sd in enumerate(sd_grid):
+            for j, ell in enumerate(ell_grid):
+                k_ff = ns["rbf"](X, X, T([0.0]), T([2.0 * math.log(ell)]))
+                big_k = k_ff + torch.eye(n) * sd ** 2                              # CP.R:45
+                kii = torch.diag(ns["chol_solve"](torch.eye(n), big_k)).view(n, 1)  # CP.R:46
+                mean_term = Y - ns["chol_solve"](Y, big_k) / kii                    # CP.R:48
+                cov_term = 1 / kii                                                  # CP.R:49
+                out[0, i, j] = ns["crps"](mean_term, cov_term, Y).item()           # CP.R:51
+                w_mean = k_ff.mm(ns["chol_solve"](Y, big_k))                        # CP.R:58
+                w_cov = torch.diag(torch.eye(n) * sd ** 2 + k_ff
+                                   - k_ff.mm(ns["chol_solve"](k_ff, big_k))).view(n, 1)  # CP.R:59
+                out[1, i, j] = ns["crps"](w_mean, w_cov, Y).item()                 # CP.R:62
+                hl = torch.linalg.cholesky(big_k, upper=True).diag().log().sum()  # log(det)/2
+                out[2, i, j] = (0.5 * Y.t().mm(ns["chol_solve"](Y, big_k)) + hl
+                                + n / 2 * math.log(2 * math.pi)).item()             # CP.R:71
+                out[3, i, j] = ns["logs"](mean_term, cov_term + sd ** 2, Y).item()  # CP.R:81-83
+    return out
+
+
 def synth(seed, n, nt, d):
     """SURVEY.md §8(d) synthetic generator."""
     rng = np.random.default_rng(seed)
@@ -537,6 +565,19 @@ def main(only=None):
         dr = np.concatenate([torch.randn(40, b).numpy().ravel() for _ in range(2)])
         dss1 = float(ns["dss"](T(m).view(-1, 1), T(C), b, T(yv).view(-1, 1)))
     save("es_single", m=m, C=C, y=yv, num_sim=40, draws=dr, es=es1, dss=dss1)
+
+    # ---- contour-plot.R surfaces: n = 20 on CP.R's 50 × 50 grid; a d = 2, n = 100 grid ----
+    sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "oracle"))
+    import gp_oracle as O  # the CP.R data generator only (x = seq(-6, 6, 20), y ~ MVN + noise)
+    x, yv = O.cp_data(seed=0)
+    l_range, sd_range = np.linspace(0.01, 2.0, 50), np.linspace(0.01, 1.0, 50)
+    save("surface_cp", x=x, y=yv, ell=l_range, sd=sd_range,
+         surf=surface_case(ns, x, yv, l_range, sd_range))
+    rng2 = np.random.default_rng(21)
+    x2 = rng2.uniform(-3, 3, (100, 2))
+    y2 = np.sin(x2[:, 0]) * np.cos(x2[:, 1]) + 0.1 * rng2.standard_normal(100)
+    l2, sd2 = np.array([0.3, 0.7, 1.1, 1.6, 2.4]), np.array([0.05, 0.2, 0.6])
+    save("surface_d2", x=x2, y=y2, ell=l2, sd=sd2, surf=surface_case(ns, x2, y2, l2, sd2))
 
     tot = 0
     for name, sz in written:

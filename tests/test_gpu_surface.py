@@ -1,0 +1,71 @@
+"""contour-plot.R objective surfaces on the GPU (gps_full_surface).
+
+Goldens: tests/golden/make_goldens.py composes CP.R:43-85 from the reference's own Python defs
+(rbf SD:8-21 with b = 2·log l, chol_solve KF:25-29, crps KF:60-68, logs KF:52-57) on CP.R's
+50 × 50 grid at n = 20 and on a d = 2, n = 100 grid.  R is absent, so R parity is unpinned;
+the data are numpy draws of CP.R's generator.  Tolerances: the whole surface normwise, against
+the movement a 1e-15 relative perturbation of x causes (measured here on the GPU).
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden, nrel
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
+
+
+@pytest.mark.parametrize("name", ["surface_cp", "surface_d2"])
+def test_surface_vs_golden(gpu_ctx, name):
+    import gpscore
+    g = load_golden(name)
+    got = gpscore.surface(g["x"], g["y"], g["ell"], g["sd"], ctx=gpu_ctx)
+    rng = np.random.default_rng(3)
+    xp = g["x"] * (1 + 1e-15 * rng.standard_normal(g["x"].shape))
+    pert = gpscore.surface(xp, g["y"], g["ell"], g["sd"], ctx=gpu_ctx)
+    for k, nm in enumerate(NAMES):
+        err = nrel(got[nm], g["surf"][k])
+        floor = nrel(pert[nm], got[nm])
+        print(f"{name} {nm:14s} gpu-vs-golden {err:.2e}  floor {floor:.2e}")
+        assert np.all(np.isfinite(got[nm]))
+        assert err <= 30 * floor + 1e-12, (nm, err, floor)
+
+
+def test_surface_matches_single_point_fits(gpu_ctx):
+    """Each grid point is the full-GP fit at that (ℓ, s): the LOO objectives and NLML equal
+    gps_full_fit's at θ = (log sf², log ℓ, log s²) (the LOO-LogS without CP.R:81's + s²)."""
+    import gpscore
+    g = load_golden("surface_d2")
+    out = gpscore.surface(g["x"], g["y"], g["ell"], g["sd"], log_sf2=0.3, logs_add_noise=False,
+                          ctx=gpu_ctx)
+    gp = gpscore.GP(ctx=gpu_ctx)
+    for i, sd in enumerate(g["sd"]):
+        for j, ell in enumerate(g["ell"]):
+            r = gp.fit(g["x"], g["y"], (0.3, np.log(ell), np.log(sd * sd)))
+            for k in ("loo_crps", "nlml", "loo_logs"):
+                assert abs(out[k][i, j] - r[k]) <= 1e-10 * max(1.0, abs(r[k])), (k, i, j)
+
+
+def test_surface_edge_cases(gpu_ctx):
+    """n = 1, n = 128 (the LDS limit), a non-PD grid point (duplicate inputs, s = 0) → NaN
+    there only, and n > 128 rejected."""
+    import gpscore
+    import gp_oracle as O
+    x1, y1 = np.array([[0.3]]), np.array([0.7])
+    s = gpscore.surface(x1, y1, [0.5, 1.0], [0.1, 0.2], ctx=gpu_ctx)
+    ref = O.cp_surface(x1, y1, [0.5, 1.0], [0.1, 0.2])
+    for k, nm in enumerate(NAMES):
+        assert nrel(s[nm], ref[k]) < 1e-13
+    rng = np.random.default_rng(1)
+    x = rng.uniform(-4, 4, (128, 3))
+    y = np.cos(x.sum(1))
+    s = gpscore.surface(x, y, [0.8, 1.5], [0.1, 0.3], ctx=gpu_ctx)
+    ref = O.cp_surface(x, y, [0.8, 1.5], [0.1, 0.3])
+    for k, nm in enumerate(NAMES):
+        assert nrel(s[nm], ref[k]) < 1e-9, (nm, nrel(s[nm], ref[k]))
+    xd = np.array([[0.0], [0.0], [1.0]])
+    s = gpscore.surface(xd, np.array([1.0, 1.0, 0.0]), [1.0], [0.0, 0.1], ctx=gpu_ctx)
+    assert np.all(np.isnan(s["nlml"][0])) and np.all(np.isfinite(s["nlml"][1]))
+    with pytest.raises(gpscore.GpsError):
+        gpscore.surface(np.zeros((129, 1)), np.zeros(129), [1.0], [0.1], ctx=gpu_ctx)

@@ -177,3 +177,14 @@ def test_es_dss_single_oracle_vs_golden():
     r = g["y"] - g["m"]
     d = 0.5 * b * O.LOG2PI + 0.5 * np.linalg.slogdet(g["C"])[1] + 0.5 * r @ np.linalg.solve(g["C"], r)
     assert abs(d - float(g["dss"])) <= 1e-12 * max(1.0, abs(float(g["dss"])))
+
+
+@pytest.mark.parametrize("name", ["surface_cp", "surface_d2"])
+def test_cp_surface_oracle_vs_golden(name):
+    """contour-plot.R surfaces (CP.R:43-85): the numpy restatement against the goldens composed
+    from the reference's own Python defs with CP.R's parameterisation (R parity unpinned: R is
+    absent; the data are numpy draws of CP.R's generator)."""
+    g = load_golden(name)
+    out = O.cp_surface(g["x"], g["y"], g["ell"], g["sd"])
+    for k in range(4):
+        assert nrel(out[k], g["surf"][k]) < 1e-9, (k, nrel(out[k], g["surf"][k]))
