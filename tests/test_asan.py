@@ -1,0 +1,43 @@
+"""Host-side AddressSanitizer pass over the C-ABI (SURVEY.md §5 "race detection / sanitizers"):
+libgpscore_asan.so (`make -C <pkg>/csrc asan`: host code under -fsanitize=address, device code
+unchanged) driven by tools/asan_check.py in a subprocess with the ASan runtime preloaded."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd")
+ASAN_LIB = os.path.join(PKG, "gpscore", "libgpscore_asan.so")
+ASAN_RT = "/opt/rocm/lib/llvm/lib/clang/22/lib/linux/libclang_rt.asan-x86_64.so"
+
+
+def _run(mode):
+    if not os.path.exists(ASAN_LIB):
+        pytest.skip("libgpscore_asan.so not built (make -C <pkg>/csrc asan; __graft_entry__.build does)")
+    rt = ASAN_RT
+    if not os.path.exists(rt):
+        rt = subprocess.run(["/opt/rocm/bin/hipcc", "-print-file-name=libclang_rt.asan-x86_64.so"],
+                            capture_output=True, text=True).stdout.strip()
+    env = dict(os.environ)
+    env["LD_PRELOAD"] = rt + ((" " + env["LD_PRELOAD"]) if env.get("LD_PRELOAD") else "")
+    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1:halt_on_error=1"
+    env["GPSCORE_LIB"] = ASAN_LIB
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asan_check.py"), mode],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-3000:])
+    assert "AddressSanitizer" not in p.stderr, p.stderr[-3000:]
+    return p.stdout
+
+
+def test_asan_null_context_paths():
+    """Every entry point with a NULL context, and context creation without a device."""
+    assert "entry points rejected" in _run("null")
+
+
+@pytest.mark.gpu
+def test_asan_device_argument_validation():
+    """A real context: invalid arguments to every entry point, then small valid fits, predicts,
+    gradients, block-LOO, FITC, compat and surface calls — all under host ASan."""
+    assert "valid paths clean" in _run("device")
