@@ -397,8 +397,10 @@ def main():
     ms_full = 1e3 * t_full / args.steps
     # kernel-accounting pass: same steps, one stream, hipEvents around every launch
     prof, ms_acct = kernel_pass(ctl, ctx, unit, args.steps)
-    obj = gp.fit(theta=th, return_loo=False).objectives
-    _, _, sc = gp.predict(with_scores=True)
+    got = gpu_unit_outputs(gp, th)  # every output of the unit, for the parity record
+    obj = {k: got[k] for k in ("nlml", "loo_crps", "loo_logs", "logdet", "quad")}
+    sc = {k: got[k] for k in ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse",
+                              "test_cover")}
 
     # HBM bytes per launch from the committed rocprofv3 counter passes
     # (tools/profile_round.sh -> tools/traffic.py; counters cannot be read live here)
@@ -546,7 +548,6 @@ def main():
         cb, ref = cpu_baseline(args.config)
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
-        got = gpu_unit_outputs(gp, th)
         res["parity"] = {"vs": f"torch-CPU ref-mirror (reference op sequence) on the same "
                                f"{args.config} inputs",
                          "metric": "normwise relative error (vectors: max|a-b|/max|b|; scalars: "

@@ -131,6 +131,8 @@ class Context:
                            f"{self.lib.gps_last_error(None).decode()}")
         self.h = h
         self.device = device
+        # which GP object's data the device currently holds, per kind ("full" / "fitc")
+        self.resident = {}
 
     def check(self, rc, what):
         if rc == 0:

@@ -68,7 +68,9 @@ class GP:
         self.ctx = ctx
         self.kind = None
         self._X = self._Z = None
+        self._Xt = self._yt = None
         self._train_key = self._test_key = self._z_key = None
+        self._token = object()  # identifies this GP's data in ctx.resident
         self.comm = None  # set by gpscore.dist.attach_comm
         self.n_total = None
         self.nt_total = None
@@ -84,6 +86,8 @@ class GP:
         self._X, self._y = X, y
         if kind == "full":
             self.ctx.call("gps_full_set_data", ptr(X), ptr(y), n, d)
+            self.ctx.resident[kind] = self._token
+            self._Xt = self._yt = None
         elif kind == "fitc":
             self.n_total = n if n_total is None else int(n_total)
             if ytr_stats is None:
@@ -91,6 +95,8 @@ class GP:
             self.ytr_stats = ytr_stats
             self.ctx.call("gps_fitc_set_data", ptr(X), ptr(y), n, d, ytr_stats[0], ytr_stats[1],
                           self.n_total)
+            self.ctx.resident[kind] = self._token
+            self._Xt = self._yt = None
             if Z is not None:
                 self.set_inducing(Z)
         else:
@@ -103,12 +109,14 @@ class GP:
         if self._X is not None and Z.shape[1] != self._X.shape[1]:
             raise ValueError("Z and X disagree on d")
         self._Z = Z
+        self._ensure_resident()
         self.ctx.call("gps_fitc_set_inducing", ptr(Z), Z.shape[0])
 
     def set_test(self, Xt, yt=None, nt_total=None):
         Xt = f64(Xt, 2)
         yt = None if yt is None else f64(yt).ravel()
         nt = Xt.shape[0]
+        self._ensure_resident()
         if self.kind == "full":
             self.ctx.call("gps_full_set_test", ptr(Xt), ptr(yt), nt)
         else:
@@ -116,6 +124,29 @@ class GP:
             self.ctx.call("gps_fitc_set_test", ptr(Xt), ptr(yt), nt, self.nt_total)
         self._nt = nt
         self._has_yt = yt is not None
+        self._Xt, self._yt = Xt, yt
+
+    def _ensure_resident(self):
+        """Several GP objects may share one context, whose device holds ONE full-GP and ONE
+        FITC data set: if another GP uploaded since, put this one's data (and inducing and
+        test points) back.  The factor of a fit is not restored — predict then needs a new
+        fit, as after any set_data."""
+        if self.kind is None or self.ctx.resident.get(self.kind) is self._token:
+            return
+        X, y, n, d = self._X, self._y, self._X.shape[0], self._X.shape[1]
+        if self.kind == "full":
+            self.ctx.call("gps_full_set_data", ptr(X), ptr(y), n, d)
+            if self._Xt is not None:
+                self.ctx.call("gps_full_set_test", ptr(self._Xt), ptr(self._yt), self._Xt.shape[0])
+        else:
+            self.ctx.call("gps_fitc_set_data", ptr(X), ptr(y), n, d, self.ytr_stats[0],
+                          self.ytr_stats[1], self.n_total)
+            if self._Z is not None:
+                self.ctx.call("gps_fitc_set_inducing", ptr(self._Z), self._Z.shape[0])
+            if self._Xt is not None:
+                self.ctx.call("gps_fitc_set_test", ptr(self._Xt), ptr(self._yt), self._Xt.shape[0],
+                              self.nt_total)
+        self.ctx.resident[self.kind] = self._token
 
     # ------------------------------------------------------------------- fit
     def fit(self, X=None, y=None, theta=(0.0, 0.0, 0.0), kind="full", Z=None, rbf=False,
@@ -129,6 +160,7 @@ class GP:
             self.set_inducing(Z)
         if self.kind is None:
             raise ValueError("no training data")
+        self._ensure_resident()
         d = self._X.shape[1]
         th, n_ell = pack_theta(theta, d)
         obj = np.zeros(5)
@@ -169,6 +201,7 @@ class GP:
             return res[0], res[1], objs
         if objective not in OBJ_NAMES[:3]:
             raise ValueError(f"objective must be one of {OBJ_NAMES[:3] + BLOCK_OBJS}")
+        self._ensure_resident()
         th, n_ell = pack_theta(theta, self._X.shape[1])
         obj = np.zeros(5)
         grad = np.zeros(2 + n_ell)
@@ -201,6 +234,7 @@ class GP:
         KF:543 / 663 — and for FITC also d/d inducing_x: (value, grad, folds, grad_Z)."""
         if objective not in BLOCK_OBJS:
             raise ValueError(f"objective must be one of {BLOCK_OBJS}")
+        self._ensure_resident()
         n, d = self._X.shape
         th, n_ell = pack_theta(theta, d)
         val = np.zeros(1)
@@ -272,6 +306,7 @@ class GP:
         spgp_cal_mean_and_cov) at Xt with the last fit's factorisation."""
         if Xt is not None:
             self.set_test(Xt, yt)
+        self._ensure_resident()
         nt = self._nt
         mu, var, sc = np.empty(nt), np.empty(nt), np.zeros(6)
         name = "gps_full_predict" if self.kind == "full" else "gps_fitc_predict"

@@ -496,3 +496,27 @@ def test_profiler_collect(gpu_ctx):
     gpu_ctx.prof(False)
     assert "potrf_diag128" in rep and "gram_kff" in rep and "gemm_trmm_colred" in rep
     assert all(v["ms"] >= 0 for v in rep.values())
+
+
+def test_gp_objects_sharing_a_context(gpu_ctx):
+    """Two GP objects on one context (the device holds one full-GP data set): each call puts
+    its own data back, so interleaved fits return each object's own objectives; a predict
+    after the other object's upload needs a new fit (the factor is not restored)."""
+    import gpscore
+    rng = np.random.default_rng(8)
+    Xa, Xb = rng.standard_normal((300, 4)), rng.standard_normal((500, 4))
+    ya, yb = np.sin(Xa.sum(1)), np.cos(Xb.sum(1))
+    th = (0.0, 0.0, np.log(0.05))
+    a, b = gpscore.GP(ctx=gpu_ctx), gpscore.GP(ctx=gpu_ctx)
+    a.set_data(Xa, ya)
+    a.set_test(Xa[:20])
+    ra = a.fit(theta=th)
+    b.set_data(Xb, yb)
+    rb = b.fit(theta=th)
+    ra2 = a.fit(theta=th)
+    assert ra2.objectives == ra.objectives and rb.objectives != ra.objectives
+    mu, _ = a.predict()
+    assert np.all(np.isfinite(mu))
+    b.fit(theta=th)
+    with pytest.raises(gpscore.GpsError, match="fit first"):
+        a.predict()
