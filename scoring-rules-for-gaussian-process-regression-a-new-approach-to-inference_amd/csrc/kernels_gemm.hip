@@ -66,26 +66,6 @@ __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int
     tj = t - r * (r + 1) / 2;
     return true;
   }
-  if (p.map_mode == 5) {
-    // XCD-banded like map 3, but the band's tiles go row by row (column by column for
-    // TRI_K_*_I), the triangular index heaviest-first inside each row: the ~64 tiles an XCD
-    // holds at once share a few operand panels of the long index (for the tall-skinny
-    // row-norm products, each A row panel is fetched once for all N / 128 tiles of its row
-    // instead of once per tile column).
-    const int x = t & 7, i = t >> 3;
-    if (p.tri == TRI_K_LE_I || p.tri == TRI_K_GE_I) {  // work follows ti: band over tj
-      const int bw = (p.tiles_n + 7) >> 3;
-      const int c = i / p.tiles_m, r = i % p.tiles_m;
-      tj = x * bw + c;
-      ti = p.tri == TRI_K_LE_I ? p.tiles_m - 1 - r : r;
-      return c < bw && tj < p.tiles_n;
-    }
-    const int bh = (p.tiles_m + 7) >> 3;  // TRI_K_LE_J / TRI_K_GE_J: band over ti
-    const int r = i / p.tiles_n, c = i % p.tiles_n;
-    ti = x * bh + r;
-    tj = p.tri == TRI_K_LE_J ? p.tiles_n - 1 - c : c;
-    return r < bh && ti < p.tiles_m;
-  }
   if (p.map_mode == 3) {
     // XCD-banded heaviest-first (triangular operands): block b runs on XCD b % 8;
     // XCD x owns a contiguous band of the index that does NOT carry the triangular
@@ -534,7 +514,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build
   if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out) q.map_mode = 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
-  if (q.map_mode == 3 || q.map_mode == 5) {
+  if (q.map_mode == 3) {
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
                                                           : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;

@@ -171,7 +171,7 @@ static int rowsq_study(double* A, double* B, double* o0) {
     {"C5/2    100032x4096", 100032, 4096}};
   GemmParams p; memset(&p, 0, sizeof(p));
   for (auto& c : cs)
-    for (int mm : {3, 5, 3, 5}) {
+    for (int mm = 0; mm < 4; ++mm) {
       p.A = A; p.B = B; p.out0 = o0; p.alpha = 1.0; p.ksplit = 1; p.tile = 0;
       p.lda = c.N; p.ldb = c.N; p.ld_out = c.M;
       p.M = c.M; p.N = c.N; p.K = c.N; p.tri = TRI_K_LE_J; p.map_mode = mm;
