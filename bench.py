@@ -152,16 +152,37 @@ def kernel_summary(prof, steps):
     return out
 
 
-def roofline_mfma(prof, traffic=None, steps=1):
+TRAFFIC_KIND = ("L2-fabric bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, gfx950 "
+                "corrections; every L2 miss, Infinity-Cache hits included: an upper bound on HBM "
+                "bytes), from the committed counter passes (tools/profile_round.sh)")
+
+
+def alg_flop(kind, c, world=1):
+    """SURVEY.md §8(d) algorithmic flops of one unit at the UNPADDED sizes: full GP
+    n³/3 (potrf) + n³/3 (trtri) + n²·n* (predictive TRMM); FITC two m×m factor+inverse
+    (4m³/3) + 3·n·m² (two row-norm TRMMs, the B SYRK) + 2·n*·m² (predict)."""
+    if kind == "full":
+        return 2.0 * c["n"] ** 3 / 3.0 + float(c["n"]) ** 2 * c["nt"]
+    # per rank: the m×m factorisations are replicated, the row work is sharded
+    return 4.0 * c["m"] ** 3 / 3.0 + (3.0 * c["n"] + 2.0 * c["nt"]) * c["m"] ** 2 / world
+
+
+def roofline_mfma(prof, traffic=None, steps=1, flop_alg=None):
+    """All GEMM launches of a step: achieved = algorithmic flops (unpadded, alg_flop) ÷ the
+    summed launch time; the padded flops the launches actually execute are reported beside."""
     f = sum(v["flop"] for k, v in prof.items() if k.startswith("gemm")) / steps
     ms = sum(v["ms"] for k, v in prof.items() if k.startswith("gemm")) / steps
     n = sum(v["count"] for k, v in prof.items() if k.startswith("gemm")) / steps
-    ach = f / (ms * 1e-3) / 1e12 if ms else 0.0
+    fa = flop_alg if flop_alg is not None else f
+    ach = fa / (ms * 1e-3) / 1e12 if ms else 0.0
     return {"bound": "mfma", "kernel": "gemm_f64_kernel (all launches of the step)",
             "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": traffic,
+            "traffic_kind": TRAFFIC_KIND if traffic is not None else None,
             "launches_per_step": n, "avg_launch_ms": ms / n if n else None,
-            "flop_per_launch": f / n if n else None}
+            "flop_per_launch": fa / n if n else None, "flop_alg_per_step": fa,
+            "flop_padded_per_step": f,
+            "achieved_at_padded_flop": round(f / (ms * 1e-3) / 1e12, 3) if ms else 0.0}
 
 
 def roofline_trailing(prof, steps=1):
@@ -184,7 +205,8 @@ def roofline_gram(prof, steps=1, traffic=None, tags=("gram_kff", "gram_ksf")):
     ach = b / (ms * 1e-3) / 1e9 if ms else 0.0
     return {"bound": "hbm", "kernel": "gram_reg_kernel<8> (K_ff lower + K*f)", "achieved": round(ach, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-            "traffic": traffic, "bytes_per_step": b,
+            "traffic": traffic, "traffic_kind": TRAFFIC_KIND if traffic is not None else None,
+            "bytes_per_step": b,
             "bytes_per_launch": b / max(1, sum(1 for t in tags if t in prof))}
 
 
@@ -367,6 +389,7 @@ def main():
     ap.add_argument("--no-tiny-gemm", action="store_true",
                     help="64-tile split-K path for the small GEMMs instead of the 16x16-per-wave kernel")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--fitc-traffic-json", default=os.path.join(ROOT, "profiles", "fitc_traffic.json"))
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
                          "no RCCL communicator (FITC objectives then cover the local shard only)")
@@ -404,13 +427,13 @@ def main():
 
     # HBM bytes per launch from the committed rocprofv3 counter passes
     # (tools/profile_round.sh -> tools/traffic.py; counters cannot be read live here)
-    traffic = traffic_gram = None
-    if os.path.exists(args.traffic_json):
+    def read_traffic(path):
         try:
-            tr = json.load(open(args.traffic_json)).get("_roofline", {})
-            traffic, traffic_gram = tr.get("gemm_per_launch_bytes"), tr.get("gram_per_launch_bytes")
-        except Exception:
-            traffic = traffic_gram = None
+            tr = json.load(open(path)).get("_roofline", {})
+            return tr.get("gemm_per_launch_bytes"), tr.get("gram_per_launch_bytes")
+        except Exception:  # noqa: BLE001 - absent / unreadable file: traffic stays null
+            return None, None
+    traffic, traffic_gram = read_traffic(args.traffic_json)
 
     res = {
         "metric": METRIC,
@@ -423,7 +446,7 @@ def main():
         "config": {"workload": f"{args.config} full GP fit(NLML+LOO-CRPS+LOO-LogS)+predict+score",
                    "n": c["n"], "d": c["d"], "n_test": c["nt"], "kernel": "ARD",
                    "parallelism": "replicas" if world > 1 else "single"},
-        "roofline": roofline_mfma(prof, traffic, args.steps),
+        "roofline": roofline_mfma(prof, traffic, args.steps, alg_flop("full", c)),
         "roofline_gram": roofline_gram(prof, args.steps, traffic_gram),
         "roofline_trailing_update": roofline_trailing(prof, args.steps),
         "objectives": obj, "scores": sc,
@@ -520,7 +543,9 @@ def main():
                                     "rows_per_rank": b - a, "ranks": world},
                          "scaling": "strong",
                          "objectives": fobj,
-                         "roofline": roofline_mfma(fprof, None, args.steps),
+                         "roofline": roofline_mfma(
+                             fprof, read_traffic(args.fitc_traffic_json)[0] if leg == "C4" else None,
+                             args.steps, alg_flop("fitc", fc, world)),
                          "kernel_accounting_ms_per_step": fms_acct,
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             if not args.no_grad:  # next-1: one FITC GD iteration (theta and Z), K20:222-247
