@@ -71,12 +71,25 @@ enum {
   GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-4 fixed orders */
   GPS_OPT_FORK_MIN = 4, /* smallest recursion block (in 128-row blocks, default 1) whose
                            off-critical-path product is forked to the side stream */
-  GPS_OPT_TINY_GEMM = 7, /* 1 (default): GEMMs with M·N <= 256² and K <= 1024 (the bottom of
-                            the recursion) use the one-wave-per-16×16-tile kernel; 0: 64-tile
-                            split-K + reduce.  Process-wide. */
+  GPS_OPT_TINY_GEMM = 7, /* 1 (default): the bottom-of-recursion GEMMs (up to the 1280 level)
+                            use the small kernel (16/32-blocks per wave, K split over the waves
+                            of a workgroup, no LDS staging, no reduce launch); 0: the 64-tile
+                            split-K + reduce path for them.  Process-wide. */
   GPS_OPT_GRAM_REG = 9,  /* 1 (default): Gram builds with d in {1, 8, 16} keep the column
                             features in registers (128×128 tiles); 0: the LDS-column kernel.
                             Bitwise-identical output.  Process-wide. */
+  GPS_OPT_GRAPH = 10,    /* 1 (default): the recursive factorisation's launch sequence is
+                            captured once per (buffers, size, streams, options) into a hipGraph
+                            and replayed; 0: eager launches.  Same kernels, same results. */
+  GPS_OPT_SIDE_MODE = 11, /* side stream of the factorisation: 0 plain (default); 1 lowest
+                             priority; 2 / 4 CU-masked to leave 16 / 32 CUs to the main stream
+                             (+1: and lowest priority).  Recreates the side stream. */
+  GPS_OPT_SIDE_PERSIST = 12, /* > 0 (multiple of 8): the side stream's GEMMs run as a persistent
+                                grid of at most this many workgroups pulling tiles from per-XCD
+                                queues; 0: one workgroup per tile. */
+  GPS_OPT_LEAF = 13,     /* 1 (default): the 128-block leaf is the MFMA kernel (16-column panels by
+                            one wave, trailing updates and the inverse on the matrix cores);
+                            0: the register-blocked VALU kernel.  Process-wide. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -92,6 +92,17 @@ struct gps_ctx {
   int ncu = 0;
   std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
   size_t sync_used = 0;
+  bool graphs = true;                  // GPS_OPT_GRAPH: replay the factorisation from a hipGraph
+  int side_mode = 0;                   // GPS_OPT_SIDE_MODE (see make_aux_streams)
+  int side_persist = 0;                // GPS_OPT_SIDE_PERSIST: resident-workgroup cap of side GEMMs
+  DBuf tctr_side;                      // their per-XCD tile counters
+  struct PotrfGraph {                  // one captured potrf_inv launch sequence
+    std::vector<uintptr_t> key;
+    hipGraphExec_t exec = nullptr;
+    uint64_t used = 0;
+  };
+  std::vector<PotrfGraph> pgraphs;     // small LRU keyed by buffers, sizes, streams, options
+  uint64_t pgraph_clock = 0;
   std::string err;
   // profiling
   int prof = 0;  // 1: per-tag timing, 2: per-shape tags
@@ -372,6 +383,10 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = Linv; p.ldb = ldl; p.C = A21; p.ldc = lda;
     p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
+    if (forked && ctx->side_persist) {  // bounded residency: the chain's launches never queue
+      p.persist = ctx->side_persist;    // behind pending workgroups of this product
+      p.tctr = static_cast<int*>(ctx->tctr_side.p);
+    }
     if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, ts))) return rc;
   }
   if (forked) HIPCHK(hipEventRecord(join, ts));
@@ -407,12 +422,65 @@ int reset_info(gps_ctx* ctx) {
   return 0;
 }
 
+// The recursion issues ~7 host calls per 128-block (launches, fork/join events): at the
+// bottom levels, where each GEMM is a few µs of GPU time, the host's ~3-4 µs per call
+// became the bound.  With GPS_OPT_GRAPH (default) the whole sequence is captured once per
+// (buffers, sizes, streams, options) into a hipGraph and replayed with one launch; the
+// eager path remains for profiling (per-launch events) and as the option's off state.
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
-  ctx->sync_used = 0;
-  int rc = potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
+  auto eager = [&]() {
+    ctx->sync_used = 0;
+    return potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
                          static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad);
-  return rc;
+  };
+  if (!ctx->graphs || ctx->prof || n_pad <= GPS_TILE) return eager();
+  const std::vector<uintptr_t> key = {
+      (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
+      (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
+      (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->gemm_map,
+      (uintptr_t)g_tiny_gemm, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
+      (uintptr_t)ctx->ws_side.p, (uintptr_t)ctx->side_persist, (uintptr_t)g_leaf_v4};
+  for (auto& g : ctx->pgraphs)
+    if (g.key == key) {
+      g.used = ++ctx->pgraph_clock;
+      HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
+      return 0;
+    }
+  // capture: everything the recursion allocates must exist beforehand (no allocation
+  // inside a capture): the split-K workspaces and the fork/join event pool
+  HIPCHK(ensure(ctx->ws_main, (size_t)kSplitWsDoubles * 8));
+  HIPCHK(ensure(ctx->ws_side, (size_t)kSplitWsDoubles * 8));
+  const size_t nev = 2 * (size_t)(n_pad / GPS_TILE) + 8;
+  while (ctx->sync_ev.size() < nev) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->sync_ev.push_back(e);
+  }
+  if (key[14] != (uintptr_t)ctx->ws_main.p || key[15] != (uintptr_t)ctx->ws_side.p)
+    return potrf_inv(ctx, A, n_pad, Linv, W, logdiag, nreal, Lout);  // key with the new buffers
+  HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  int rc = eager();
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+  if (rc || ec != hipSuccess) {
+    if (graph) (void)hipGraphDestroy(graph);
+    if (rc) return rc;
+    HIPCHK(ec);
+  }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  HIPCHK(ei);
+  if (ctx->pgraphs.size() >= 8) {  // evict the least recently used
+    auto lru = std::min_element(ctx->pgraphs.begin(), ctx->pgraphs.end(),
+                                [](const auto& a, const auto& b) { return a.used < b.used; });
+    (void)hipGraphExecDestroy(lru->exec);
+    ctx->pgraphs.erase(lru);
+  }
+  ctx->pgraphs.push_back({key, exec, ++ctx->pgraph_clock});
+  HIPCHK(hipGraphLaunch(exec, ctx->stream));
+  return 0;
 }
 
 int check_info(gps_ctx* ctx) {
@@ -897,8 +965,24 @@ int gps_version(void) { return 100; }
 // the off-critical-path streams: side (T products of the factorisation) and aux[0..1]
 // (with side, the concurrent energy-score folds)
 int make_aux_streams(gps_ctx* ctx) {
-  for (hipStream_t* a : {&ctx->side, &ctx->aux[0], &ctx->aux[1]})
+  for (hipStream_t* a : {&ctx->aux[0], &ctx->aux[1]})
     HIPCHK(hipStreamCreateWithFlags(a, hipStreamNonBlocking));
+  // side stream (the factorisation's off-critical-path T products): side_mode bit 0 = lowest
+  // stream priority; bits 1-2 = CU mask leaving 16 / 32 CUs (the highest-numbered) to the
+  // main stream's latency-bound chain (A/B experiment, GPS_OPT_SIDE_MODE)
+  const int mode = ctx->side_mode;
+  int least = 0, greatest = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  const int reserve = (mode >> 1) & 3 ? 16 * ((mode >> 1) & 3) : 0;
+  if (reserve && ctx->ncu > reserve) {
+    std::vector<uint32_t> mask((ctx->ncu + 31) / 32, 0u);
+    for (int c = 0; c < ctx->ncu - reserve; ++c) mask[c / 32] |= 1u << (c % 32);
+    HIPCHK(hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mask.size(), mask.data()));
+  } else if (mode & 1) {
+    HIPCHK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  }
   return 0;
 }
 
@@ -947,6 +1031,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
+  for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (hipStream_t l : ctx->aux)
     if (l) (void)hipStreamDestroy(l);
@@ -981,6 +1066,24 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
+    case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
+    case GPS_OPT_LEAF: g_leaf_v4 = value != 0; return 0;
+    case GPS_OPT_SIDE_PERSIST:
+      ARGCHK(value >= 0 && value % 8 == 0, "GPS_OPT_SIDE_PERSIST: a multiple of 8");
+      HIPCHK(ensure(ctx->tctr_side, 8 * 64));
+      ctx->side_persist = value;
+      return 0;
+    case GPS_OPT_SIDE_MODE: {  // recreate the side stream (drop graphs captured on the old one)
+      HIPCHK(hipDeviceSynchronize());
+      for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
+      ctx->pgraphs.clear();
+      for (hipStream_t* a : {&ctx->side, &ctx->aux[0], &ctx->aux[1]}) {
+        if (*a) HIPCHK(hipStreamDestroy(*a));
+        *a = nullptr;
+      }
+      ctx->side_mode = value;
+      return make_aux_streams(ctx);
+    }
     default: return fail(ctx, -1, "unknown option");
   }
 }

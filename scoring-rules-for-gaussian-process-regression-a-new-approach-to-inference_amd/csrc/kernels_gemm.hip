@@ -109,7 +109,50 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 }
 
 template <int ALAY, int BLAY, int EPI, int TILE>
+__device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
+                                          double* smem);
+
+template <int ALAY, int BLAY, int EPI, int TILE>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
+  constexpr int LS = TILE + 16;          // LDS row stride (doubles)
+  constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
+  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
+  // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
+
+  if (p.persist) {
+    // persistent grid (a bounded number of resident workgroups, so a concurrent stream's
+    // dispatches never queue behind pending workgroups of this launch): tiles are pulled
+    // from per-XCD counters in the same per-XCD order the dispatch-order grid would give
+    // (virtual block vb runs on XCD vb % 8), then stolen from the other XCDs' queues
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    __shared__ int pull;
+    for (int q = 0; q < 8; ++q) {
+      const int x = (xcc + q) & 7;
+      for (;;) {
+        __syncthreads();  // the previous tile's LDS reads are done before pull / smem change
+        if (tid == 0) pull = atomicAdd(p.tctr + 16 * x, 1);
+        __syncthreads();
+        const int vb = x + 8 * pull;
+        if (vb >= p.nvb) break;
+        int ti, tj;
+        if (tile_of(p, remap ? xcd_remap(vb, p.nvb) : vb, ti, tj))
+          gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, 0, smem);
+      }
+    }
+    return;
+  }
+  int ti, tj;
+  if (!tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj)) return;
+  gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, blockIdx.y, smem);
+}
+
+template <int ALAY, int BLAY, int EPI, int TILE>
+__device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
+                                          double* smem) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
   constexpr int WT = TILE / 2;           // per-wave sub-tile edge
@@ -120,14 +163,8 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
                                          // owns NQ 16-byte chunks 2·TPR doubles apart, so a
                                          // ds_write_b128 covers contiguous bytes: no conflicts)
   constexpr int TPI = BK / PER;          // threads per i-row for i-major sources
-  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-
-  int ti, tj;
-  const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
-  // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
-  if (!tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj)) return;
   const int row0 = ti * TILE, col0 = tj * TILE;
 
   int kb = 0, ke = p.K;
@@ -144,7 +181,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   }
   if (p.ksplit > 1) {
     const int nk = ke > kb ? (ke - kb) / BK : 0;
-    const int s = blockIdx.y, q = nk / p.ksplit, r = nk % p.ksplit;
+    const int s = kslice, q = nk / p.ksplit, r = nk % p.ksplit;
     const int s0 = s * q + min(s, r), s1 = s0 + q + (s < r ? 1 : 0);
     ke = kb + s1 * BK;
     kb = kb + s0 * BK;
@@ -260,7 +297,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
 
   const int lrow = lane >> 4, lcol = lane & 15;
   if constexpr (EPI == EPI_STORE) {
-    double* Cb = p.C + (int64_t)blockIdx.y * p.c_kslice_stride;
+    double* Cb = p.C + (int64_t)kslice * p.c_kslice_stride;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -330,99 +367,167 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   }
 }
 
-// Latency-optimised GEMM for the bottom of the recursion (M·N <= 256², K <= 1024): one
-// wave per 16×16 output tile, operands streamed straight from L2 into MFMA registers (no
-// LDS, no K split, no reduction launch).  For 16-deep K chunks lane l (r = l & 15,
+// Latency-optimised GEMM for the bottom of the recursion: no LDS staging, no split-K slabs,
+// no reduction launch.  A wave owns a (16R)×(16R) output block (R·R accumulators of
+// v_mfma_f64_16x16x4) over its share of K; WPT waves of one workgroup split K between them
+// and the partial sums meet in LDS (fixed order: bitwise reproducible).  Operands stream
+// straight from L2 into MFMA registers: for a 16-deep K chunk lane l (r = l & 15,
 // g = l >> 4) feeds MFMA step kk with k = 4g + kk of A row r and B column r — a fixed
-// permutation of k inside the chunk shared by both operands, so row-major A / Bᵀ
-// fragments are one contiguous 32-byte load per lane.  Chain per wave: K/4 MFMAs (32 at
-// K = 128, ~0.9 µs) against ~11 µs for the 64-tile split-K kernel + ordered reduce.
-// lower_out enumerates the 16-tiles of the lower 64-tiles (diagonal 64-tiles whole, as
-// the 64/128-tile kernels write them).
-template <int ALAY, int BLAY>
-__global__ __launch_bounds__(256) void gemm_f64_tiny_kernel(GemmParams p) {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int tm = p.M / 16, tn = p.N / 16;
-  int ti, tj;
-  if (p.lower_out) {  // 16-tiles (ti, tj) with tj/4 <= ti/4, row-major over ti
-    // rows of 16-tiles ti contain 4·(ti/4 + 1) tiles; prefix S(ti) = 4·Σ_{q<ti}(q/4 + 1)
-    int lo = 0, hi = tm;
-    auto pre = [](int r) { const int a = r / 4, b = r % 4; return 4 * (4 * a * (a + 1) / 2 + b * (a + 1)); };
-    if (t >= pre(tm)) return;
-    while (hi - lo > 1) { const int mid = (lo + hi) / 2; if (pre(mid) <= t) lo = mid; else hi = mid; }
-    ti = lo;
-    tj = t - pre(ti);
+// permutation of k inside the chunk shared by both operands, so row-major A / Bᵀ fragments
+// are one contiguous 32-byte load per lane.  Loads are issued G chunks at a time, one group
+// ahead of the MFMAs, so a K range of ≤ G chunks per wave costs ONE memory latency (the
+// one-chunk-ahead predecessor paid one per chunk: ~6-7 µs at K = 128, profiles/r2_kernel_stats).
+// lower_out enumerates the blocks of the lower 64-tiles (diagonal 64-tiles whole, as the
+// 64/128-tile kernels write them).
+template <int ALAY, int BLAY, int R, int WPT>
+__global__ __launch_bounds__(256) void gemm_f64_small_kernel(GemmParams p) {
+  constexpr int TE = 16 * R;         // output block edge per tile
+  constexpr int TPB = 4 / WPT;       // tiles per workgroup
+  constexpr int G = R == 1 ? 4 : 2;  // 16-deep chunks per load group (64 VGPRs per group)
+  constexpr int NACC = R * R * 4;    // doubles of accumulator per lane
+  __shared__ double red[WPT > 1 ? 4 * NACC * 64 : 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = wave / WPT, part = wave - slot * WPT;
+  const int t = blockIdx.x * TPB + slot;
+  const int tm = p.M / TE, tn = p.N / TE;
+  int ti = 0, tj = 0;
+  bool valid;
+  if (p.lower_out) {  // blocks (ti, tj) with tj/u <= ti/u, u = 64/TE, row-major over ti
+    constexpr int u = 64 / TE;
+    auto pre = [](int r) { const int a = r / u, b = r % u; return u * (u * a * (a + 1) / 2 + b * (a + 1)); };
+    valid = t < pre(tm);
+    if (valid) {
+      int lo = 0, hi = tm;
+      while (hi - lo > 1) { const int mid = (lo + hi) / 2; if (pre(mid) <= t) lo = mid; else hi = mid; }
+      ti = lo;
+      tj = t - pre(ti);
+    }
   } else {
-    if (t >= tm * tn) return;
-    ti = t / tn;
-    tj = t - ti * tn;
+    valid = t < tm * tn;
+    if (valid) { ti = t / tn; tj = t - ti * tn; }
   }
-  const int row0 = ti * 16, col0 = tj * 16;
+  if (WPT == 1 && !valid) return;  // (with WPT > 1 every wave reaches the LDS barrier)
+  const int row0 = ti * TE, col0 = tj * TE;
   int kb = 0, ke = p.K;
   switch (p.tri) {
-    case TRI_K_LE_I: ke = min(ke, row0 + 16); break;
-    case TRI_K_LE_J: ke = min(ke, col0 + 16); break;
+    case TRI_K_LE_I: ke = min(ke, row0 + TE); break;
+    case TRI_K_LE_J: ke = min(ke, col0 + TE); break;
     case TRI_K_GE_J: kb = col0; break;
     case TRI_K_GE_I: kb = row0; break;
     case TRI_KR_J:
       kb = p.kr[2 * (col0 / 16)];
-      ke = p.kr[2 * (col0 / 16) + 1];
+      ke = p.kr[2 * ((col0 + TE) / 16 - 1) + 1];
       break;
     default: break;
   }
+  const int nk = valid && ke > kb ? (ke - kb) / 16 : 0;
+  const int q = nk / WPT, rr = nk - q * WPT;
+  const int c0 = part * q + min(part, rr), c1 = c0 + q + (part < rr ? 1 : 0);
   const int r = lane & 15, g = lane >> 4;
-  auto load = [&](int k0, double (&a)[4], double (&b)[4]) {
-    const int k = k0 + 4 * g;
-    if constexpr (ALAY == LAY_N) {
-      const dv2* s = reinterpret_cast<const dv2*>(p.A + (int64_t)(row0 + r) * p.lda + k);
-      const dv2 u = s[0], v = s[1];
-      a[0] = u.x; a[1] = u.y; a[2] = v.x; a[3] = v.y;
-    } else {
+
+  typedef double Frag[G][R][4];
+  auto load_chunk = [&](int c, double (&a)[R][4], double (&b)[R][4]) {
+    const int k = kb + 16 * c + 4 * g;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = p.A[(int64_t)(k + q) * p.lda + row0 + r];
-    }
-    if constexpr (BLAY == LAY_T) {
-      const dv2* s = reinterpret_cast<const dv2*>(p.B + (int64_t)(col0 + r) * p.ldb + k);
-      const dv2 u = s[0], v = s[1];
-      b[0] = u.x; b[1] = u.y; b[2] = v.x; b[3] = v.y;
-    } else {
+    for (int i = 0; i < R; ++i) {
+      const int row = row0 + 16 * i + r;
+      if constexpr (ALAY == LAY_N) {
+        const dv2* s = reinterpret_cast<const dv2*>(p.A + (int64_t)row * p.lda + k);
+        const dv2 u0 = s[0], u1 = s[1];
+        a[i][0] = u0.x; a[i][1] = u0.y; a[i][2] = u1.x; a[i][3] = u1.y;
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = p.B[(int64_t)(k + q) * p.ldb + col0 + r];
+        for (int e = 0; e < 4; ++e) a[i][e] = p.A[(int64_t)(k + e) * p.lda + row];
+      }
+      const int col = col0 + 16 * i + r;
+      if constexpr (BLAY == LAY_T) {
+        const dv2* s = reinterpret_cast<const dv2*>(p.B + (int64_t)col * p.ldb + k);
+        const dv2 u0 = s[0], u1 = s[1];
+        b[i][0] = u0.x; b[i][1] = u0.y; b[i][2] = u1.x; b[i][3] = u1.y;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[i][e] = p.B[(int64_t)(k + e) * p.ldb + col];
+      }
     }
   };
-  d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
-  double a0[4], b0[4], a1[4], b1[4];
-  int k0 = kb;
-  if (k0 < ke) load(k0, a0, b0);
-  while (k0 < ke) {
-    const bool more = k0 + 16 < ke;
-    if (more) load(k0 + 16, a1, b1);
+  d4 acc[R][R];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[kk], b0[kk], acc, 0, 0, 0);
-    k0 += 16;
-    if (!more) break;
-    const bool more2 = k0 + 16 < ke;
-    if (more2) load(k0 + 16, a0, b0);
+  for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[kk], b1[kk], acc, 0, 0, 0);
-    k0 += 16;
-    if (!more2) break;
+    for (int j = 0; j < R; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  auto load_group = [&](int c, Frag& a, Frag& b) {
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (c + j < c1) load_chunk(c + j, a[j], b[j]);
+  };
+  auto mma_group = [&](int c, const Frag& a, const Frag& b) {
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (c + j < c1) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int jj = 0; jj < R; ++jj)
+              acc[i][jj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j][i][kk], b[j][jj][kk], acc[i][jj], 0, 0, 0);
+      }
+  };
+  Frag fa0, fb0, fa1, fb1;
+  int c = c0;
+  if (c < c1) load_group(c, fa0, fb0);
+  while (c < c1) {
+    if (c + G < c1) load_group(c + G, fa1, fb1);
+    mma_group(c, fa0, fb0);
+    c += G;
+    if (c >= c1) break;
+    if (c + G < c1) load_group(c + G, fa0, fb0);
+    mma_group(c, fa1, fb1);
+    c += G;
+  }
+  if constexpr (WPT > 1) {  // partial sums of the K parts meet in LDS, summed in part order
+    double* mine = red + (int64_t)wave * NACC * 64 + lane;
+    if (part > 0) {
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mine[((i * R + j) * 4 + e) * 64] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (part > 0 || !valid) return;
+#pragma unroll
+    for (int w = 1; w < WPT; ++w) {
+      const double* o = mine + w * NACC * 64;
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] += o[((i * R + j) * 4 + e) * 64];
+    }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    double* c = p.C + (int64_t)(row0 + g + 4 * q) * p.ldc + col0 + r;
-    double v = p.alpha * acc[q];
-    if (p.beta != 0.0) v = fma(p.beta, *c, v);
-    *c = v;
-  }
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      double* crow = p.C + (int64_t)(row0 + 16 * i + g + 4 * e) * p.ldc + col0 + r;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double v = p.alpha * acc[i][j][e];
+        if (p.beta != 0.0) v = fma(p.beta, crow[16 * j], v);
+        crow[16 * j] = v;
+      }
+    }
 }
 
-static int64_t tiny_tiles(const GemmParams& p) {
-  const int64_t tm = p.M / 16, tn = p.N / 16;
+// output blocks of the small kernel at edge te (lower_out: the blocks of the lower 64-tiles)
+static int64_t small_tiles(const GemmParams& p, int te) {
+  const int64_t tm = p.M / te, tn = p.N / te;
   if (!p.lower_out) return tm * tn;
-  const int64_t a = tm / 4;  // lower 64-tiles, 16 sub-tiles each (M multiple of 128)
-  return 16 * a * (a + 1) / 2;
+  const int64_t u = 64 / te, a = tm / u;
+  return u * u * a * (a + 1) / 2;
 }
 
 // C = beta*C + alpha * sum_s slab_s, slabs summed in slice order (deterministic);
@@ -446,6 +551,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
 
+// waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
+static int small_wpt(int K) { return K >= 64 ? 4 : (K >= 32 ? 2 : 1); }
+
 static int64_t tiles_for(const GemmParams& p, int tile) {
   const int64_t tm = p.M / tile, tn = p.N / tile;
   return p.lower_out ? tm * (tm + 1) / 2 : tm * tn;
@@ -459,10 +567,21 @@ static int64_t tiles_for(const GemmParams& p, int tile) {
 // (their partial sums are laid out per 128-tile).  Thresholds from the
 // tools/gemm_bench.cpp sweep on MI355X (profiles/r1_gemm_sweep.txt): e.g. a
 // 1280-level triangular product 161 us -> 58 us, 2560-level 31 -> 47 TF/s.
+// The bottom of the recursion goes to the small kernel (profiles/r2_small_gemm.txt,
+// per launch incl. the boundary): 16-blocks up to M·N = 256² (128³: 7.6 -> 3.4 µs),
+// 32-blocks for triangular products up to the 1280 level (640³ 23.5 -> 15-19 µs,
+// 1024³ 45 -> 35 µs) and for SYRKs up to 640 (640² K=640 17.1 -> 14.2 µs); the
+// LDS-tiled 64-tile kernel stays ahead for larger SYRKs (less L2 traffic per flop).
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap) {
   if (p.tile) return {p.tile, p.ksplit > 1 ? p.ksplit : 1};
   if (epi != EPI_STORE || p.ksplit > 1) return {128, p.ksplit > 1 ? p.ksplit : 1};
-  if (g_tiny_gemm && !p.kscale && (int64_t)p.M * p.N <= 256 * 256 && p.K <= 1024) return {16, 1};
+  if (g_tiny_gemm && !p.kscale && p.K <= 1280) {
+    const int64_t mn = (int64_t)p.M * p.N;
+    if ((mn <= 256 * 256 && p.K <= 1024) || (p.lower_out && p.M <= 384 && p.K <= 640))
+      return {16, small_wpt(p.K)};
+    if (p.lower_out ? (p.M <= 640 && p.K <= 640) : (mn <= 1280 * 1280 && (p.tri || p.K <= 640)))
+      return {32, small_wpt(p.K)};
+  }
   if (tiles_for(p, 128) >= 1024) return {128, 1};
   const int64_t t64 = tiles_for(p, 64);
   const int64_t target = p.lower_out ? 2048 : 1024;
@@ -482,14 +601,26 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   if (p.ksplit < 1) p.ksplit = 1;
   const GemmPlan plan = gemm_plan(epi, p, p.ws ? p.ws_cap : 0);
   const int tile = plan.tile;
-  if (tile == 16) {
-    const int64_t tt = tiny_tiles(p);
-    const dim3 grid((unsigned)((tt + 3) / 4)), block(256);
-    if (alay == LAY_N && blay == LAY_T) hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_N, LAY_T>), grid, block, 0, s, p);
-    else if (alay == LAY_N && blay == LAY_N) hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_N, LAY_N>), grid, block, 0, s, p);
-    else if (alay == LAY_T && blay == LAY_N) hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_T, LAY_N>), grid, block, 0, s, p);
-    else hipLaunchKernelGGL((gemm_f64_tiny_kernel<LAY_T, LAY_T>), grid, block, 0, s, p);
-    return hipGetLastError();
+  if (tile == 16 || tile == 32) {  // small kernel: tile = block edge, ksplit = waves per block
+    if (epi != EPI_STORE || p.kscale) return hipErrorInvalidValue;
+    const int wpt = plan.ksplit;
+    if (wpt != 1 && wpt != 2 && wpt != 4) return hipErrorInvalidValue;
+    const int64_t tt = small_tiles(p, tile);
+    const dim3 grid((unsigned)((tt * wpt + 3) / 4)), block(256);
+    hipError_t err = hipErrorInvalidValue;
+#define GPS_SMALL_CASE(AL, BL, RR, W)                                                           \
+    if (err == hipErrorInvalidValue && alay == AL && blay == BL && tile == 16 * RR && wpt == W) { \
+      hipLaunchKernelGGL((gemm_f64_small_kernel<AL, BL, RR, W>), grid, block, 0, s, p);           \
+      err = hipGetLastError();                                                                    \
+    }
+#define GPS_SMALL_LAYOUTS(RR, W)                                                                \
+    GPS_SMALL_CASE(LAY_N, LAY_T, RR, W) GPS_SMALL_CASE(LAY_N, LAY_N, RR, W)                     \
+    GPS_SMALL_CASE(LAY_T, LAY_N, RR, W) GPS_SMALL_CASE(LAY_T, LAY_T, RR, W)
+    GPS_SMALL_LAYOUTS(1, 1) GPS_SMALL_LAYOUTS(1, 2) GPS_SMALL_LAYOUTS(1, 4)
+    GPS_SMALL_LAYOUTS(2, 1) GPS_SMALL_LAYOUTS(2, 2) GPS_SMALL_LAYOUTS(2, 4)
+#undef GPS_SMALL_LAYOUTS
+#undef GPS_SMALL_CASE
+    return err;
   }
   if (tile != 64 && tile != 128) return hipErrorInvalidValue;
   if (tile == 64 && epi != EPI_STORE) return hipErrorInvalidValue;
@@ -518,6 +649,14 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
                                                           : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;
+  }
+  q.nvb = tiles;
+  if (q.persist > 0 && (q.persist & 7) == 0 && q.tctr && q.ksplit == 1 && tiles > q.persist) {
+    const hipError_t em = hipMemsetAsync(q.tctr, 0, 8 * 64, s);
+    if (em != hipSuccess) return em;
+    tiles = q.persist;
+  } else {
+    q.persist = 0;
   }
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
+GPS_OPT_GRAPH, GPS_OPT_SIDE_MODE, GPS_OPT_SIDE_PERSIST, GPS_OPT_LEAF = 10, 11, 12, 13
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
 GPS_SURF_LOGS_ADD_NOISE = 1
@@ -171,14 +172,20 @@ class Context:
         self.call("gps_ctx_set_option", GPS_OPT_OVERLAP, 1 if on else 0)
 
     def set_tiny_gemm(self, on=True):
-        """One-wave-per-16×16 kernel for the small GEMMs at the bottom of the recursion
-        (default) or the 64-tile split-K path (process-wide)."""
+        """The small kernel (16/32-blocks per wave, K split across a workgroup's waves) for
+        the GEMMs at the bottom of the recursion (default) or the 64-tile split-K path
+        (process-wide)."""
         self.call("gps_ctx_set_option", GPS_OPT_TINY_GEMM, 1 if on else 0)
 
     def set_gram_reg(self, on=True):
         """Register-resident Gram kernel for d in {1, 8, 16} (default) or the LDS-column
         kernel; bitwise-identical output (process-wide)."""
         self.call("gps_ctx_set_option", GPS_OPT_GRAM_REG, 1 if on else 0)
+
+    def set_graphs(self, on=True):
+        """Replay the recursive factorisation from a captured hipGraph (default) or launch
+        it eagerly."""
+        self.call("gps_ctx_set_option", GPS_OPT_GRAPH, 1 if on else 0)
 
     def synchronize(self):
         self.call("gps_ctx_synchronize")

@@ -2,7 +2,8 @@
 ~5% in GEMM clocks, so variants must be compared inside one run).
 
   python tools/ab_bench.py --config C3 map=0 map=4 ov=0
-  options: map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN)
+  options: map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN),
+           graph (GPS_OPT_GRAPH), tiny (GPS_OPT_TINY_GEMM)
 Variants are interleaved round-robin for --rounds rounds; prints the median ms/unit.
 """
 import argparse
@@ -20,7 +21,9 @@ import bench  # noqa: E402
 import gpscore  # noqa: E402
 from gpscore import _lib  # noqa: E402
 
-KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN}
+KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN,
+        "graph": _lib.GPS_OPT_GRAPH, "tiny": _lib.GPS_OPT_TINY_GEMM, "side": _lib.GPS_OPT_SIDE_MODE,
+        "persist": _lib.GPS_OPT_SIDE_PERSIST, "leaf": _lib.GPS_OPT_LEAF}
 
 
 def main():

@@ -1,5 +1,7 @@
-// Timing + correctness of the 128×128 leaf kernel (potrf + inverse): the library's kernel
-// (csrc/kernels_potrf.hip) against the MFMA-tiled experiment (tools/leaf_mfma.hip), same box.
+// Timing + correctness of the 128×128 leaf kernel (potrf + inverse): the library's v4 MFMA leaf
+// and v3 register-blocked leaf (csrc/kernels_potrf.hip, g_leaf_v4) and the round-2 MFMA-tiled
+// experiment (tools/leaf_mfma.hip), same box.  Also: NaN in the strict upper triangle of the
+// input must not change any output (the kernels read the lower triangle only).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -68,6 +70,27 @@ static int run(const char* name, LeafFn launch_potrf_diag) {
   hipEventRecord(e1); hipEventSynchronize(e1);
   hipEventElapsedTime(&ms, e0, e1);
   printf("%.2f us per diag block (with Lout)\n", 1e3 * ms / reps);
+  // NaN above the diagonal: outputs unchanged
+  {
+    std::vector<double> hn(h);
+    for (int i = 0; i < n; ++i)
+      for (int j = i + 1; j < n; ++j) hn[i * n + j] = nan("");
+    hipMemcpy(A, hn.data(), n * n * 8, hipMemcpyHostToDevice);
+    hipMemset(info, 0x7f, 4);
+    launch_potrf_diag(A, n, Li, n, Lo, n, ld, info, 0, n, 0);
+    std::vector<double> nLi(n * n), nLo(n * n);
+    hipMemcpy(nLi.data(), Li, n * n * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(nLo.data(), Lo, n * n * 8, hipMemcpyDeviceToHost);
+    int ninfo; hipMemcpy(&ninfo, info, 4, hipMemcpyDeviceToHost);
+    double d = 0.0;
+    for (int i = 0; i < n * n; ++i) {
+      if (!(nLi[i] == gLi[i]) || !(nLo[i] == gLo[i])) d = 1.0;
+    }
+    printf("NaN-upper input: outputs %s, info %s\n", d == 0.0 ? "bitwise equal" : "DIFFER",
+           ninfo == 0x7f7f7f7f ? "untouched" : "SET");
+    if (d != 0.0 || ninfo != 0x7f7f7f7f) eL = 1.0;
+    hipMemcpy(A, h.data(), n * n * 8, hipMemcpyHostToDevice);
+  }
   // non-PD pivot at row 77: info must be 78
   h[77 * n + 77] = -1.0;
   hipMemcpy(A, h.data(), n * n * 8, hipMemcpyHostToDevice);
@@ -81,8 +104,29 @@ static int run(const char* name, LeafFn launch_potrf_diag) {
   return ok ? 0 : 1;
 }
 
+static void print_stamps() {
+#ifdef GPS_V4_STAMPS
+  long long st[4][40];
+  hipMemcpyFromSymbol(st, HIP_SYMBOL(v4::g_v4_stamps), sizeof(st));
+  const long long t0 = st[0][0];
+  printf("v4 stamps (cycles from start): load done w0 %lld w1 %lld\n", st[0][1] - t0, st[1][1] - t0);
+  for (int p = 0; p < 8; ++p)
+    printf("  p=%d  A-end w0 %6lld w1 %6lld w2 %6lld w3 %6lld | B-start %6lld | B-end w1 %6lld w2 %6lld w3 %6lld | next %6lld\n", p,
+           st[0][2 + 4 * p] - t0, st[1][2 + 4 * p] - t0, st[2][2 + 4 * p] - t0, st[3][2 + 4 * p] - t0,
+           st[0][3 + 4 * p] - t0, st[1][4 + 4 * p] - t0, st[2][4 + 4 * p] - t0, st[3][4 + 4 * p] - t0,
+           st[0][5 + 4 * p] - t0);
+  for (int w = 0; w < 4; ++w)
+    printf("  tail w%d: T done %lld, barrier %lld, finish %lld, end %lld\n", w, st[w][37] - t0,
+           st[w][38] - t0, st[w][39] - t0, st[w][36] - t0);
+#endif
+}
+
 int main(int argc, char** argv) {
-  int rc = run("library leaf (kernels_potrf.hip)", launch_potrf_leaf);
+  g_leaf_v4 = 1;
+  int rc = run("library leaf v4 (MFMA, kernels_potrf.hip)", launch_potrf_leaf);
+  print_stamps();
+  g_leaf_v4 = 0;
+  rc |= run("library leaf v3 (register-blocked, kernels_potrf.hip)", launch_potrf_leaf);
   if (argc < 2 || strcmp(argv[1], "lib") != 0) rc |= run("MFMA-tiled leaf (tools/leaf_mfma.hip)", launch_potrf_leaf_mfma);
   return rc;
 }

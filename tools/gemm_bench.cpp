@@ -88,6 +88,88 @@ static int sweep(double* A, double* B, double* C, double* ws) {
   return 0;
 }
 
+// small-kernel study: the recursion's small shapes under the grouped-prefetch small kernel
+// (block edge 16/32 × waves per block 1/2/4) against the 64-tile split-K plans; every variant
+// is checked against the 128-tile single-slice result (max |diff|)
+__global__ void maxdiff_kernel(const double* a, const double* b, int64_t n, int ncol, int lower, double* out) {
+  double m = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (!lower || (i % ncol) / 64 <= (i / ncol) / 64) m = fmax(m, fabs(a[i] - b[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) out[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = m;
+}
+static double maxdiff(const double* a, const double* b, int64_t n, int ncol, int lower) {
+  static double* d = nullptr;
+  if (!d) hipMalloc(&d, 256 * 4 * 8);
+  maxdiff_kernel<<<256, 256>>>(a, b, n, ncol, lower, d);
+  double h[1024];
+  hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  double m = 0.0;
+  for (double v : h) m = fmax(m, v);
+  return m;
+}
+static int small_study(double* A, double* B, double* C, double* ws) {
+  struct S { const char* name; int M, N, K, al, bl, tri, lower; } cs[] = {
+    {"L128 tri1 NN", 128, 128, 128, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L128 tri2 NT", 128, 128, 128, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L128 tri3 NN", 128, 128, 128, LAY_N, LAY_N, TRI_K_GE_J, 0},
+    {"L128 syrk", 128, 128, 128, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L256 tri1 NN", 256, 128, 256, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L256 syrk", 256, 256, 128, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L256sq tri2 NT", 256, 256, 256, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L384 tri1 NN", 384, 256, 384, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L384 tri2 NT", 384, 256, 256, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L384 syrk", 384, 384, 256, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L512 tri2 NT", 512, 512, 512, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L512 syrk", 512, 512, 512, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L640 tri1 NN", 640, 640, 640, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L640 tri2 NT", 640, 640, 640, LAY_N, LAY_T, TRI_K_LE_J, 0},
+    {"L640 tri3 NN", 640, 640, 640, LAY_N, LAY_N, TRI_K_GE_J, 0},
+    {"L640 syrk", 640, 640, 640, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L1k tri1 NN", 1024, 1024, 1024, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L1k syrk", 1024, 1024, 1024, LAY_N, LAY_T, TRI_NONE, 1},
+    {"L1280 tri1 NN", 1280, 1152, 1280, LAY_N, LAY_N, TRI_K_LE_I, 0},
+    {"L1280 syrk", 1280, 1280, 1152, LAY_N, LAY_T, TRI_NONE, 1},
+  };
+  double* Cref;
+  if (hipMalloc(&Cref, (int64_t)2048 * 2048 * 8) != hipSuccess) return 1;
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (auto& c : cs) {
+    p.A = A; p.B = B; p.ws = ws; p.ws_cap = 1ll << 28;
+    p.lda = c.al == LAY_N ? c.K : c.M;
+    p.ldb = c.bl == LAY_T ? c.K : c.N;
+    p.ldc = c.N;
+    p.M = c.M; p.N = c.N; p.K = c.K; p.tri = c.tri; p.lower_out = c.lower;
+    p.alpha = -1.0; p.beta = 0.0;
+    const double fl = c.lower ? (double)c.M * (c.M + 1) * c.K : (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.K;
+    const int reps = 200;
+    hipMemset(Cref, 0, (size_t)c.M * c.N * 8);
+    p.C = Cref; p.tile = 128; p.ksplit = 1;
+    launch_gemm(c.al, c.bl, EPI_STORE, p, 0);
+    p.C = C;
+    p.tile = 0; p.ksplit = 1;
+    const GemmPlan ap = gemm_plan(EPI_STORE, p, p.ws_cap);
+    double t = run(c.al, c.bl, EPI_STORE, p, reps, fl);
+    printf("%-15s auto(t%d,k%d) %6.1fus |", c.name, ap.tile, ap.ksplit, fl / (t * 1e12) * 1e6);
+    for (int tile : {64}) for (int ks : {1, 2, 4, 8}) {
+      if (c.K / ks < 64) continue;
+      p.tile = tile; p.ksplit = ks;
+      t = run(c.al, c.bl, EPI_STORE, p, reps, fl);
+      printf(" t64/k%d %6.1f", ks, fl / (t * 1e12) * 1e6);
+    }
+    printf(" |");
+    for (int tile : {16, 32}) for (int w : {1, 2, 4}) {
+      p.tile = tile; p.ksplit = w;
+      hipMemset(C, 0, (size_t)c.M * c.N * 8);
+      t = run(c.al, c.bl, EPI_STORE, p, reps, fl);
+      const double d = maxdiff(C, Cref, (int64_t)c.M * c.N, c.N, c.lower);
+      printf(" s%d/w%d %6.1f%s", tile, w, fl / (t * 1e12) * 1e6, d > 1e-9 ? "(BAD)" : "");
+    }
+    printf("\n");
+  }
+  return 0;
+}
+
 // leading-dimension study: the 10k-level shapes of the C3 build with the operands'
 // real leading dimension (n_pad = 20096) against compact and padded alternatives
 static int ldstudy(double* A, double* B, double* C) {
@@ -195,6 +277,10 @@ int main(int argc, char** argv) {
   hipMemset(w, 0, n * 8);
   printf("operands: %s\n", zeros ? "zeros" : "uniform random [-0.5, 0.5)");
   if (argc > 1 && !strcmp(argv[1], "ld")) return ldstudy(A, B, C);
+  if (argc > 1 && !strcmp(argv[1], "small")) {
+    double* ws; hipMalloc(&ws, (int64_t)8 << 28);
+    return small_study(A, B, C, ws);
+  }
   if (argc > 1 && !strcmp(argv[1], "syrk")) return syrk_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "layout")) return layout_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "rowsq")) return rowsq_study(A, B, o0);
