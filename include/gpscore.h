@@ -81,15 +81,6 @@ enum {
   GPS_OPT_GRAPH = 10,    /* 1 (default): the recursive factorisation's launch sequence is
                             captured once per (buffers, size, streams, options) into a hipGraph
                             and replayed; 0: eager launches.  Same kernels, same results. */
-  GPS_OPT_SIDE_MODE = 11, /* side stream of the factorisation: 0 plain (default); 1 lowest
-                             priority; 2 / 4 CU-masked to leave 16 / 32 CUs to the main stream
-                             (+1: and lowest priority).  Recreates the side stream. */
-  GPS_OPT_SIDE_PERSIST = 12, /* > 0 (multiple of 8): the side stream's GEMMs run as a persistent
-                                grid of at most this many workgroups pulling tiles from per-XCD
-                                queues; 0: one workgroup per tile. */
-  GPS_OPT_LEAF = 13,     /* 1 (default): the 128-block leaf is the MFMA kernel (16-column panels by
-                            one wave, trailing updates and the inverse on the matrix cores);
-                            0: the register-blocked VALU kernel.  Process-wide. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -93,9 +93,6 @@ struct gps_ctx {
   std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
   size_t sync_used = 0;
   bool graphs = true;                  // GPS_OPT_GRAPH: replay the factorisation from a hipGraph
-  int side_mode = 0;                   // GPS_OPT_SIDE_MODE (see make_aux_streams)
-  int side_persist = 0;                // GPS_OPT_SIDE_PERSIST: resident-workgroup cap of side GEMMs
-  DBuf tctr_side;                      // their per-XCD tile counters
   struct PotrfGraph {                  // one captured potrf_inv launch sequence
     std::vector<uintptr_t> key;
     hipGraphExec_t exec = nullptr;
@@ -383,10 +380,6 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = Linv; p.ldb = ldl; p.C = A21; p.ldc = lda;
     p.M = n2; p.N = n1; p.K = n1; p.tri = TRI_K_GE_J;
-    if (forked && ctx->side_persist) {  // bounded residency: the chain's launches never queue
-      p.persist = ctx->side_persist;    // behind pending workgroups of this product
-      p.tctr = static_cast<int*>(ctx->tctr_side.p);
-    }
     if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, ts))) return rc;
   }
   if (forked) HIPCHK(hipEventRecord(join, ts));
@@ -440,7 +433,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
       (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->gemm_map,
       (uintptr_t)g_tiny_gemm, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
-      (uintptr_t)ctx->ws_side.p, (uintptr_t)ctx->side_persist, (uintptr_t)g_leaf_v4};
+      (uintptr_t)ctx->ws_side.p};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       g.used = ++ctx->pgraph_clock;
@@ -965,27 +958,10 @@ int gps_version(void) { return 100; }
 // the off-critical-path streams: side (T products of the factorisation) and aux[0..1]
 // (with side, the concurrent energy-score folds)
 int make_aux_streams(gps_ctx* ctx) {
-  for (hipStream_t* a : {&ctx->aux[0], &ctx->aux[1]})
+  for (hipStream_t* a : {&ctx->side, &ctx->aux[0], &ctx->aux[1]})
     HIPCHK(hipStreamCreateWithFlags(a, hipStreamNonBlocking));
-  // side stream (the factorisation's off-critical-path T products): side_mode bit 0 = lowest
-  // stream priority; bits 1-2 = CU mask leaving 16 / 32 CUs (the highest-numbered) to the
-  // main stream's latency-bound chain (A/B experiment, GPS_OPT_SIDE_MODE)
-  const int mode = ctx->side_mode;
-  int least = 0, greatest = 0;
-  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  const int reserve = (mode >> 1) & 3 ? 16 * ((mode >> 1) & 3) : 0;
-  if (reserve && ctx->ncu > reserve) {
-    std::vector<uint32_t> mask((ctx->ncu + 31) / 32, 0u);
-    for (int c = 0; c < ctx->ncu - reserve; ++c) mask[c / 32] |= 1u << (c % 32);
-    HIPCHK(hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mask.size(), mask.data()));
-  } else if (mode & 1) {
-    HIPCHK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
-  } else {
-    HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-  }
   return 0;
 }
-
 int gps_ctx_create(int device, gps_ctx** out) {
   gps_ctx* ctx = nullptr;
   if (!out) return fail(nullptr, -1, "out is NULL");
@@ -1067,23 +1043,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
-    case GPS_OPT_LEAF: g_leaf_v4 = value != 0; return 0;
-    case GPS_OPT_SIDE_PERSIST:
-      ARGCHK(value >= 0 && value % 8 == 0, "GPS_OPT_SIDE_PERSIST: a multiple of 8");
-      HIPCHK(ensure(ctx->tctr_side, 8 * 64));
-      ctx->side_persist = value;
-      return 0;
-    case GPS_OPT_SIDE_MODE: {  // recreate the side stream (drop graphs captured on the old one)
-      HIPCHK(hipDeviceSynchronize());
-      for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
-      ctx->pgraphs.clear();
-      for (hipStream_t* a : {&ctx->side, &ctx->aux[0], &ctx->aux[1]}) {
-        if (*a) HIPCHK(hipStreamDestroy(*a));
-        *a = nullptr;
-      }
-      ctx->side_mode = value;
-      return make_aux_streams(ctx);
-    }
     default: return fail(ctx, -1, "unknown option");
   }
 }

@@ -65,16 +65,12 @@ struct GemmParams {
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
-  int persist;               // > 0: at most this many resident workgroups (multiple of 8) pull
-  int* tctr;                 //   tiles from 8 per-XCD counters (tctr, zeroed per launch, 64 B apart)
-  int nvb;                   //   virtual grid (set by launch_gemm)
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
 struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
-extern int g_leaf_v4;    // 1: the v4 MFMA leaf (kernels_potrf.hip), 0: the v3 register-blocked leaf
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 
 // ------------------------------------------------------------ device reductions

@@ -117,34 +117,9 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
-  const int tid = threadIdx.x;
   const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
   // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
 
-  if (p.persist) {
-    // persistent grid (a bounded number of resident workgroups, so a concurrent stream's
-    // dispatches never queue behind pending workgroups of this launch): tiles are pulled
-    // from per-XCD counters in the same per-XCD order the dispatch-order grid would give
-    // (virtual block vb runs on XCD vb % 8), then stolen from the other XCDs' queues
-    int xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7;
-    __shared__ int pull;
-    for (int q = 0; q < 8; ++q) {
-      const int x = (xcc + q) & 7;
-      for (;;) {
-        __syncthreads();  // the previous tile's LDS reads are done before pull / smem change
-        if (tid == 0) pull = atomicAdd(p.tctr + 16 * x, 1);
-        __syncthreads();
-        const int vb = x + 8 * pull;
-        if (vb >= p.nvb) break;
-        int ti, tj;
-        if (tile_of(p, remap ? xcd_remap(vb, p.nvb) : vb, ti, tj))
-          gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, 0, smem);
-      }
-    }
-    return;
-  }
   int ti, tj;
   if (!tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj)) return;
   gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, blockIdx.y, smem);
@@ -649,14 +624,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
                                                           : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;
-  }
-  q.nvb = tiles;
-  if (q.persist > 0 && (q.persist & 7) == 0 && q.tctr && q.ksplit == 1 && tiles > q.persist) {
-    const hipError_t em = hipMemsetAsync(q.tctr, 0, 8 * 64, s);
-    if (em != hipSuccess) return em;
-    tiles = q.persist;
-  } else {
-    q.persist = 0;
   }
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
-GPS_OPT_GRAPH, GPS_OPT_SIDE_MODE, GPS_OPT_SIDE_PERSIST, GPS_OPT_LEAF = 10, 11, 12, 13
+GPS_OPT_GRAPH = 10
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
 GPS_SURF_LOGS_ADD_NOISE = 1

@@ -22,8 +22,7 @@ import gpscore  # noqa: E402
 from gpscore import _lib  # noqa: E402
 
 KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN,
-        "graph": _lib.GPS_OPT_GRAPH, "tiny": _lib.GPS_OPT_TINY_GEMM, "side": _lib.GPS_OPT_SIDE_MODE,
-        "persist": _lib.GPS_OPT_SIDE_PERSIST, "leaf": _lib.GPS_OPT_LEAF}
+        "graph": _lib.GPS_OPT_GRAPH, "tiny": _lib.GPS_OPT_TINY_GEMM}
 
 
 def main():

@@ -1,6 +1,6 @@
 // Timing + correctness of the 128×128 leaf kernel (potrf + inverse): the library's v4 MFMA leaf
-// and v3 register-blocked leaf (csrc/kernels_potrf.hip, g_leaf_v4) and the round-2 MFMA-tiled
-// experiment (tools/leaf_mfma.hip), same box.  Also: NaN in the strict upper triangle of the
+// (csrc/kernels_potrf.hip), the round-1 register-blocked v3 leaf (tools/leaf_v3.hip) and the
+// first MFMA-tiled experiment (tools/leaf_mfma.hip), same box.  Also: NaN in the strict upper triangle of the
 // input must not change any output (the kernels read the lower triangle only).
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <vector>
 #include "kernels_potrf.hip"
+#include "leaf_v3.hip"
 #include "leaf_mfma.hip"
 using namespace gps;
 typedef hipError_t (*LeafFn)(const double*, int64_t, double*, int64_t, double*, int64_t, double*,
@@ -122,11 +123,9 @@ static void print_stamps() {
 }
 
 int main(int argc, char** argv) {
-  g_leaf_v4 = 1;
   int rc = run("library leaf v4 (MFMA, kernels_potrf.hip)", launch_potrf_leaf);
   print_stamps();
-  g_leaf_v4 = 0;
-  rc |= run("library leaf v3 (register-blocked, kernels_potrf.hip)", launch_potrf_leaf);
+  rc |= run("round-1 leaf v3 (register-blocked, tools/leaf_v3.hip)", leafv3::launch_potrf_leaf_v3);
   if (argc < 2 || strcmp(argv[1], "lib") != 0) rc |= run("MFMA-tiled leaf (tools/leaf_mfma.hip)", launch_potrf_leaf_mfma);
   return rc;
 }
