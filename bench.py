@@ -158,13 +158,13 @@ TRAFFIC_KIND = ("L2-fabric bytes per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, 
 
 
 def alg_flop(kind, c, world=1):
-    """SURVEY.md §8(d) algorithmic flops of one unit at the UNPADDED sizes: full GP
-    n³/3 (potrf) + n³/3 (trtri) + n²·n* (predictive TRMM); FITC two m×m factor+inverse
-    (4m³/3) + 3·n·m² (two row-norm TRMMs, the B SYRK) + 2·n*·m² (predict)."""
+    """BASELINE.md §"Unit and roofline" algorithmic flops of one unit at the UNPADDED sizes:
+    full GP n³/3 (potrf) + n³/3 (trtri) + n²·n* (predictive TRMM); FITC 2m³/3 (the two m×m
+    factorisations) + 3·n·m² (two row-norm TRMMs, the B SYRK) + 2·n*·m² (predict)."""
     if kind == "full":
         return 2.0 * c["n"] ** 3 / 3.0 + float(c["n"]) ** 2 * c["nt"]
     # per rank: the m×m factorisations are replicated, the row work is sharded
-    return 4.0 * c["m"] ** 3 / 3.0 + (3.0 * c["n"] + 2.0 * c["nt"]) * c["m"] ** 2 / world
+    return 2.0 * c["m"] ** 3 / 3.0 + (3.0 * c["n"] + 2.0 * c["nt"]) * c["m"] ** 2 / world
 
 
 def roofline_mfma(prof, traffic=None, steps=1, flop_alg=None):

@@ -136,6 +136,10 @@ struct gps_ctx {
   int fd = 0;
   double f_ytr_mean = 0, f_ytr_var = 1;
   bool f_data = false, f_test = false, f_z = false, f_fitted = false;
+  // test-side ‖Lm⁻¹k_*‖² formed by gps_fitc_fit on aux[0] during Lb's factorisation
+  bool f_pre = false;
+  hipEvent_t pre_fork = nullptr, pre_join = nullptr;
+  DBuf fslab_pre;
   Theta fth;
   // ---- comm: RCCL (gps_comm_init) or the in-process group (gps_comm_init_local)
   ncclComm_t comm = nullptr;
@@ -302,7 +306,7 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
 
 int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp, int m, int d,
          const Theta& th, double diag_add, int lower, int pad_identity, double* out, int64_t ldo,
-         int M, int N) {
+         int M, int N, hipStream_t st = nullptr) {
   GramParams g;
   memset(&g, 0, sizeof(g));
   g.x = x;
@@ -320,8 +324,8 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
   g.pad_identity = pad_identity;
   for (int k = 0; k < d; ++k) g.inv_ell[k] = th.inv_ell[k];
   const double elems = lower ? 0.5 * (double)M * (M + 1) : (double)M * N;
-  Prof pr(ctx, tag, 0, 8.0 * elems);
-  HIPCHK(launch_gram(g, ctx->stream));
+  Prof pr(ctx, tag, 0, 8.0 * elems, st);
+  HIPCHK(launch_gram(g, st ? st : ctx->stream));
   return 0;
 }
 
@@ -997,7 +1001,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
                  &ctx->Z, &ctx->Kmm, &ctx->Am, &ctx->Lm, &ctx->Lb, &ctx->ldm, &ctx->ldb,
                  &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
-                 &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->t0,
+                 &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->fslab_pre, &ctx->t0,
                  &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_aux[0], &ctx->ws_aux[1],
                  &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
@@ -1007,6 +1011,8 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (DBuf* b : all) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join})
+    if (e) (void)hipEventDestroy(e);
   for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (hipStream_t l : ctx->aux)
@@ -1262,6 +1268,7 @@ int gps_full_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n,
   if (int rc = bind(ctx)) return rc;
   ARGCHK(X && y && n > 1 && d >= 1 && d <= GPS_MAX_D, "bad training data");
   ARGCHK(n <= (int64_t)1 << 30, "n too large");
+  if (d != ctx->d) ctx->have_test = false;  // a test set of another input dimension is void
   ctx->n = n;
   ctx->d = d;
   ctx->n_pad = pad_to(n);
@@ -1498,6 +1505,7 @@ int gps_fitc_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n,
                       double ytr_mean, double ytr_var_unbiased, int64_t n_total) {
   if (int rc = bind(ctx)) return rc;
   ARGCHK(X && y && n > 0 && d >= 1 && d <= GPS_MAX_D && n_total >= n, "bad FITC training data");
+  if (d != ctx->fd) ctx->f_test = ctx->f_z = false;  // test set / inducing points of another d
   ctx->fn = n;
   ctx->fd = d;
   ctx->fn_pad = pad_to(n);
@@ -1508,6 +1516,7 @@ int gps_fitc_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n,
   if (int rc = upload(ctx, ctx->fy, y, n, 1, ctx->fn_pad)) return rc;
   ctx->f_data = true;
   ctx->f_fitted = false;
+  ctx->f_pre = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1525,6 +1534,7 @@ int gps_fitc_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t 
   if (!yt) zeros.assign(std::max<int64_t>(nt, 1), 0.0);
   if (int rc = upload(ctx, ctx->fyt, yt ? yt : zeros.data(), nt, 1, ctx->fnt_pad)) return rc;
   ctx->f_test = true;
+  ctx->f_pre = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1538,6 +1548,7 @@ int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m) {
   if (int rc = upload(ctx, ctx->Z, Z, m, ctx->fd, ctx->m_pad)) return rc;
   ctx->f_z = true;
   ctx->f_fitted = false;
+  ctx->f_pre = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1574,10 +1585,44 @@ int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* ds
   return 0;
 }
 
-// forward FITC objectives; leaves Knm, Lm⁻¹, Lb⁻¹, λ, r, g = Knm c, c on the device
-int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ]) {
+// Test-side half of the FITC predict that depends only on θ, Z and Lm: K*m and
+// q*_i = ‖Lm⁻¹k*_i‖² (spgp_cal_mean_and_cov K20:76-83).  gps_fitc_fit launches it on aux[0]
+// just before B's factorisation, whose latency-bound chain leaves most CUs idle; predict
+// waits on the join event instead of recomputing (measured in DESIGN.md §7).
+int fitc_test_prepass(gps_ctx* ctx) {
+  const Theta& th = ctx->fth;
+  const int64_t nt = ctx->fnt, ntp = ctx->fnt_pad, m = ctx->m, mp = ctx->m_pad;
+  const int64_t tm = mp / GPS_TILE;
+  hipStream_t a = ctx->aux[0];
+  HIPCHK(ensure(ctx->Ksm, (size_t)ntp * mp * 8));
+  HIPCHK(ensure(ctx->qm, ntp * 8));
+  HIPCHK(ensure(ctx->fslab_pre, (size_t)tm * ntp * 8));
+  for (hipEvent_t* e : {&ctx->pre_fork, &ctx->pre_join})
+    if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ctx->pre_fork, ctx->stream));
+  HIPCHK(hipStreamWaitEvent(a, ctx->pre_fork, 0));
+  int rc;
+  if ((rc = gram(ctx, "gram_ksm", ctx->fXt.d(), (int)nt, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
+                 ctx->Ksm.d(), mp, (int)ntp, (int)mp, a)))
+    return rc;
+  GemmParams p = gp0();
+  p.A = ctx->Ksm.d(); p.lda = mp; p.B = ctx->Lm.d(); p.ldb = mp;
+  p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+  p.out0 = ctx->fslab_pre.d(); p.ld_out = ntp;
+  if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, a))) return rc;
+  HIPCHK(launch_slab_sum(ctx->fslab_pre.d(), ntp, (int)tm, ntp, nullptr, ctx->qm.d(), a));
+  HIPCHK(hipEventRecord(ctx->pre_join, a));
+  ctx->f_pre = true;
+  return 0;
+}
+
+// forward FITC objectives; leaves Knm, Lm⁻¹, Lb⁻¹, λ, r, g = Knm c, c on the device.
+// pre_test: also form the test-side Lm row norms during B's factorisation (gps_fitc_fit)
+int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
+                  bool pre_test = false) {
   ARGCHK(ctx->f_data && ctx->f_z, "gps_fitc_set_data / gps_fitc_set_inducing first");
   ctx->f_fitted = false;  // set again by the callers once check_info has passed
+  ctx->f_pre = false;
   if (int rc = set_theta(ctx, ctx->fth, GPS_ARD, theta, n_ell, ctx->fd)) return rc;
   const Theta& th = ctx->fth;
   const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
@@ -1659,6 +1704,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     Prof pr(ctx, "allreduce_B", 0, 8.0 * (blen + mp + 2));
     if ((rc = allreduce_sum(ctx, red, (size_t)(blen + mp + 2), s))) return rc;
   }
+  if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
+    if ((rc = fitc_test_prepass(ctx))) return rc;
   // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
   if (shard)
     HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
@@ -1689,6 +1736,9 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                            ctx->fmu_loo.d(), ctx->fvar_loo.d(), scal + 2, s));
   }
   if ((rc = allreduce_sum(ctx, scal + 2, 2, s))) return rc;
+  // the pre-pass reads the test inputs: it is done before this call returns (it finished long
+  // before on the timeline — B's factorisation and the r pass came after its launch)
+  if (ctx->f_pre) HIPCHK(hipStreamWaitEvent(s, ctx->pre_join, 0));
   HIPCHK(hipMemcpyAsync(ctx->hsmall, scal, 4 * 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(ctx->hsmall + 4, sm, 3 * 8, hipMemcpyDeviceToHost, s));
   if ((rc = check_info(ctx))) return rc;
@@ -1709,7 +1759,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
 int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
                  double* mu_loo, double* var_loo) {
   if (int rc = bind(ctx)) return rc;
-  if (int rc = fitc_fit_core(ctx, theta, n_ell, obj)) return rc;
+  if (int rc = fitc_fit_core(ctx, theta, n_ell, obj, true)) return rc;
   const int64_t n = ctx->fn;
   hipStream_t s = ctx->stream;
   if (mu_loo) HIPCHK(hipMemcpyAsync(mu_loo, ctx->fmu_loo.p, n * 8, hipMemcpyDeviceToHost, s));
@@ -2335,12 +2385,16 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   HIPCHK(ensure(ctx->fslab, std::max(ctx->fslab.cap, (size_t)tm * ntp * 8)));
   double* sums = ctx->small.d() + 8;
   int rc;
-  if ((rc = gram(ctx, "gram_ksm", ctx->fXt.d(), (int)nt, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
-                 ctx->Ksm.d(), mp, (int)ntp, (int)mp)))
+  const bool pre = ctx->f_pre;  // K*m and q* came with the fit (fitc_test_prepass)
+  if (pre) {
+    HIPCHK(hipStreamWaitEvent(s, ctx->pre_join, 0));
+  } else if ((rc = gram(ctx, "gram_ksm", ctx->fXt.d(), (int)nt, ctx->Z.d(), (int)m, ctx->fd, th,
+                        0.0, 0, 0, ctx->Ksm.d(), mp, (int)ntp, (int)mp))) {
     return rc;
+  }
   const double* Ls[2] = {ctx->Lm.d(), ctx->Lb.d()};
   double* outs[2] = {ctx->qm.d(), ctx->qb.d()};
-  for (int w = 0; w < 2; ++w) {
+  for (int w = pre ? 1 : 0; w < 2; ++w) {
     GemmParams p = gp0();
     p.A = ctx->Ksm.d(); p.lda = mp; p.B = Ls[w]; p.ldb = mp;
     p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;

@@ -284,6 +284,42 @@ def test_stream_schedules_agree(gp, gpu_ctx):
     assert nrel(r0.mu_loo, f["loo_mu"]) < 1e-9 and abs(r0.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
+def test_new_input_dimension_voids_test_set(gpu_ctx):
+    """set_data with another input dimension drops the resident test set (and, for FITC, the
+    inducing points) at the C-ABI: predict / fit then report what is missing instead of
+    reading the old d-wide inputs with the new d (which ran off the end of the buffer).  Also
+    covers the FITC test pre-pass that gps_fitc_fit launches when a test set is resident."""
+    import gpscore
+    from gpscore._lib import ptr
+    rng = np.random.default_rng(4)
+    th8 = np.array([0.0, 0.3, np.log(0.01)])
+    X8, Xt8, y8 = rng.standard_normal((300, 8)), rng.standard_normal((1000, 8)), rng.standard_normal(300)
+    X16, y16 = rng.standard_normal((300, 16)), rng.standard_normal(300)
+    out = np.zeros(8)
+    for kind in ("full", "fitc"):
+        c = gpu_ctx
+        if kind == "full":
+            c.call("gps_full_set_data", ptr(X8), ptr(y8), 300, 8)
+            c.call("gps_full_set_test", ptr(Xt8), None, 1000)
+            c.call("gps_full_set_data", ptr(X16), ptr(y16), 300, 16)
+            c.call("gps_full_fit", 0, ptr(th8), 1, ptr(out), None, None)
+            with pytest.raises(gpscore.GpsError, match="set_test"):
+                c.call("gps_full_predict", None, None, None)
+        else:
+            c.call("gps_fitc_set_data", ptr(X8), ptr(y8), 300, 8, 0.0, 1.0, 300)
+            c.call("gps_fitc_set_inducing", ptr(X8[:40]), 40)
+            c.call("gps_fitc_set_test", ptr(Xt8), None, 1000, 1000)
+            c.call("gps_fitc_fit", ptr(th8), 1, ptr(out), None, None)
+            c.call("gps_fitc_set_data", ptr(X16), ptr(y16), 300, 16, 0.0, 1.0, 300)
+            with pytest.raises(gpscore.GpsError, match="set_inducing"):
+                c.call("gps_fitc_fit", ptr(th8), 1, ptr(out), None, None)
+            c.call("gps_fitc_set_inducing", ptr(X16[:40]), 40)
+            c.call("gps_fitc_fit", ptr(th8), 1, ptr(out), None, None)  # no test set: no pre-pass
+            with pytest.raises(gpscore.GpsError, match="set_test"):
+                c.call("gps_fitc_predict", None, None, None)
+    c.synchronize()
+
+
 def test_failed_fit_clears_factor(gpu_ctx):
     """A fit that fails (non-PD / NaN factor) after a successful one leaves no stale factor
     behind: predict then reports an error instead of returning numbers from the failed
