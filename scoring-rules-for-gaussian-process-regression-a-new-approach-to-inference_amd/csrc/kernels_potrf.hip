@@ -158,8 +158,11 @@ __device__ __forceinline__ void invert_diag(double* S, double* DG, int p, int la
 #ifdef GPS_V4_STAMPS
 __device__ long long g_v4_stamps[4][40];  // [wave][event]: tools/diag_bench.cpp timing build only
 #define V4_STAMP(ev) do { if (lane == 0) g_v4_stamps[wave][ev] = __builtin_amdgcn_s_memtime(); } while (0)
+__device__ long long g_v4_pstamps[8][3];  // wave 0 per panel: loaded, factored, stored
+#define V4_PSTAMP(p, ev) do { if (lane == 0) g_v4_pstamps[p][ev] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define V4_STAMP(ev) do { } while (0)
+#define V4_PSTAMP(p, ev) do { } while (0)
 #endif
 // tile row of lower tile t (t = i(i+1)/2 + j)
 __device__ __forceinline__ constexpr int tile_i(int t) {
@@ -241,8 +244,10 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
 #pragma unroll
         for (int c = 0; c < 16; ++c) P[s][c] = R >= t0 ? S[t + c] : 0.0;
       }
+      V4_PSTAMP(p, 0);
       if (p < 4) factor_panel<0, true>(P, p, lane, M);
       else factor_panel<1, false>(P, p, lane, M);
+      V4_PSTAMP(p, 1);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int R = lane + 64 * s;
@@ -258,6 +263,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
             dst[c] = R >= t0 ? (dv2){P[s][2 * c], P[s][2 * c + 1]} : (dv2){0.0, 0.0};
         }
       }
+      V4_PSTAMP(p, 2);
     } else if (p >= 1) {
       const int pp = p - 1;
       // wave 1 + pp % 3 inverts L_{pp,pp} (and takes the logs); the bulk tiles go to the

@@ -20,7 +20,7 @@ def cls(name, grid):
 rows = []
 for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
-                 int(r["Stream_Id"]), int(r["Queue_Id"]), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"])))
+                 int(r["Queue_Id"]), int(r["Queue_Id"]), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"])))
 rows.sort()
 kff = [i for i, k in enumerate(rows) if "gram_reg_kernel<8>" in k[2] and k[5] > 5_000_000]
 u = int(sys.argv[2]) if len(sys.argv) > 2 else 1
@@ -35,7 +35,7 @@ for k in win:
 main = max(streams, key=lambda s: len(streams[s]))
 for s, ks in sorted(streams.items()):
     busy = sum(e - st for st, e, *_ in ks)
-    print("stream %d%s: %d kernels, busy %.3f ms" % (s, " (main)" if s == main else "", len(ks), busy / 1e6))
+    print("queue %d%s: %d kernels, busy %.3f ms" % (s, " (main)" if s == main else "", len(ks), busy / 1e6))
 ks = streams[main]
 dur = defaultdict(float)
 cnt = defaultdict(int)
@@ -52,7 +52,7 @@ lv = sorted((e - st) / 1e3 for st, e, nm, *_ in ks if "potrf_diag" in nm)
 if lv:
     print("leaves: %d, median %.1f us, sum %.3f ms, the 5 longest: %s" % (
         len(lv), lv[len(lv) // 2], sum(lv) / 1e3, " ".join("%.0f" % v for v in lv[-5:])))
-print("main stream: busy %.3f ms, gaps %.3f ms" % (sum(dur.values()) / 1e6, tot_gap / 1e6))
+print("main queue: busy %.3f ms, gaps %.3f ms" % (sum(dur.values()) / 1e6, tot_gap / 1e6))
 print("%-34s %6s %10s %10s %9s" % ("class", "n", "busy ms", "gap ms", "avg us"))
 for c in sorted(dur, key=lambda c: -(dur[c] + gap_before[c])):
     print("%-34s %6d %10.3f %10.3f %9.1f" % (c[:34], cnt[c], dur[c] / 1e6, gap_before[c] / 1e6,

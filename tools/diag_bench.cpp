@@ -116,6 +116,11 @@ static void print_stamps() {
            st[0][2 + 4 * p] - t0, st[1][2 + 4 * p] - t0, st[2][2 + 4 * p] - t0, st[3][2 + 4 * p] - t0,
            st[0][3 + 4 * p] - t0, st[1][4 + 4 * p] - t0, st[2][4 + 4 * p] - t0, st[3][4 + 4 * p] - t0,
            st[0][5 + 4 * p] - t0);
+  long long ps[8][3];
+  hipMemcpyFromSymbol(ps, HIP_SYMBOL(v4::g_v4_pstamps), sizeof(ps));
+  for (int p = 0; p < 8; ++p)
+    printf("  pivot p=%d: load %lld, factor %lld, store %lld cycles\n", p,
+           ps[p][0] - (p ? st[0][5 + 4 * (p - 1)] : st[0][1]), ps[p][1] - ps[p][0], ps[p][2] - ps[p][1]);
   for (int w = 0; w < 4; ++w)
     printf("  tail w%d: T done %lld, barrier %lld, finish %lld, end %lld\n", w, st[w][37] - t0,
            st[w][38] - t0, st[w][39] - t0, st[w][36] - t0);
