@@ -138,6 +138,14 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
                                          // owns NQ 16-byte chunks 2·TPR doubles apart, so a
                                          // ds_write_b128 covers contiguous bytes: no conflicts)
   constexpr int TPI = BK / PER;          // threads per i-row for i-major sources
+  // Image row k starts 4·(k >> 2) doubles in (skew SK on both images): the lanes that transpose
+  // one i-major source row store to k rows PER apart, which the skew puts on different banks
+  // (2-way / 4-way conflicts on every transposing store without it); the 4 rows one MFMA step
+  // reads share a skew, so fragment reads stay conflict-free.  Applied where it measured faster
+  // (profiles/r2_lds_skew_ab.txt): NT +1-5 % and every 64-tile shape +3-6 %; NN -2-5 % and
+  // TN -1 % at TILE = 128, which keep the plain images.
+  constexpr bool SK = TILE == 64 || (ALAY == LAY_N && BLAY == LAY_T);
+  auto rowoff = [](int k) { return k * LS + (SK ? 4 * (k >> 2) : 0); };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int row0 = ti * TILE, col0 = tj * TILE;
@@ -207,25 +215,25 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     if constexpr (ALAY == LAY_T) {
       const int k = tid / TPR, i = (tid % TPR) * 2;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *reinterpret_cast<dv2*>(&As[k * LS + i + 2 * TPR * q]) = ra[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<dv2*>(&As[rowoff(k) + i + 2 * TPR * q]) = ra[q];
     } else {
       const int i = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        As[(k + 2 * q) * LS + i] = ra[q].x;
-        As[(k + 2 * q + 1) * LS + i] = ra[q].y;
+        As[rowoff(k + 2 * q) + i] = ra[q].x;
+        As[rowoff(k + 2 * q + 1) + i] = ra[q].y;
       }
     }
     if constexpr (BLAY == LAY_N) {
       const int k = tid / TPR, j = (tid % TPR) * 2;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) *reinterpret_cast<dv2*>(&Bs[k * LS + j + 2 * TPR * q]) = rb[q];
+      for (int q = 0; q < NQ; ++q) *reinterpret_cast<dv2*>(&Bs[rowoff(k) + j + 2 * TPR * q]) = rb[q];
     } else {
       const int j = tid / TPI, k = (tid % TPI) * PER;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        Bs[(k + 2 * q) * LS + j] = rb[q].x;
-        Bs[(k + 2 * q + 1) * LS + j] = rb[q].y;
+        Bs[rowoff(k + 2 * q) + j] = rb[q].x;
+        Bs[rowoff(k + 2 * q + 1) + j] = rb[q].y;
       }
     }
   };
@@ -241,7 +249,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     const double* Bs = As + BK * LS;
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
-      const int krow = (kk * 4 + (lane >> 4)) * LS + (lane & 15);
+      const int krow = rowoff(kk * 4 + (lane >> 4)) + (lane & 15);
       double a[MI], b[MI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) a[mi] = As[krow + wr * WT + mi * 16];
