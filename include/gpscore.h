@@ -81,6 +81,10 @@ enum {
   GPS_OPT_GRAPH = 10,    /* 1 (default): the recursive factorisation's launch sequence is
                             captured once per (buffers, size, streams, options) into a hipGraph
                             and replayed; 0: eager launches.  Same kernels, same results. */
+  GPS_OPT_PRED_PRE = 11, /* 1 (default): gps_fitc_fit forms the row-norm columns
+                            q_i = ‖Lm⁻¹k_i‖² that need only the top-level Lm11⁻¹ (a quarter of
+                            the pass) on a second stream while the rest of Lm's factorisation
+                            runs; 0: the whole pass after it.  Same tiles, same results. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -78,6 +78,8 @@ std::map<long long, std::weak_ptr<LocalGroup>> g_groups;
 
 }  // namespace
 
+enum { PRE_NONE = 0, PRE_FITC_Q = 1 };
+
 struct gps_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -93,6 +95,13 @@ struct gps_ctx {
   std::vector<hipEvent_t> sync_ev;     // fork/join events (timing disabled)
   size_t sync_used = 0;
   bool graphs = true;                  // GPS_OPT_GRAPH: replay the factorisation from a hipGraph
+  bool pred_pre = true;                // GPS_OPT_PRED_PRE
+  struct PrePass {                     // work potrf_inv launches on aux[0] once the top-level
+    int kind = 0;                      // L11⁻¹ is final: PRE_FITC_Q (the q column tiles [0, n1))
+    int64_t n1 = 0;
+    const double* L = nullptr;         // the top-level L⁻¹
+    hipEvent_t join = nullptr;         // waited by the top-level call before it returns
+  } pre;
   struct PotrfGraph {                  // one captured potrf_inv launch sequence
     std::vector<uintptr_t> key;
     hipGraphExec_t exec = nullptr;
@@ -113,7 +122,7 @@ struct gps_ctx {
   DBuf info, small;
   // ---- full GP state
   DBuf X, y, Xt, yt, A, Linv, W, logdiag, beta, alpha, dinv, slab, mu_loo, var_loo, Ksf, s1, s2,
-      mu, var, Lout;
+      mu, var, Lout, pslab;
   size_t linv_zeroed = 0;
   int n_ell = 1;
   DBuf gu, gct, gv, Mx, gslab, gout;  // gradient scratch
@@ -273,6 +282,12 @@ double gemm_flops(const GemmParams& p) {
     return 2.0 * GPS_TILE * f;
   }
   if (p.lower_out) return M * (M + 1) * K;  // SYRK, lower half
+  if ((p.tri == TRI_K_LE_I || p.tri == TRI_K_LE_J) && p.tri_off) {
+    // rows (K_LE_I) / columns (K_LE_J) [off, off + len) of a larger triangular product
+    const double len = p.tri == TRI_K_LE_I ? M : N, other = p.tri == TRI_K_LE_I ? N : M;
+    const double o = p.tri_off, e = std::min<double>(K, o + len);
+    return other * (e * e - o * o) + 2.0 * other * K * std::max(0.0, o + len - e);
+  }
   if (p.tri) return M * N * K;              // triangular operand: half of 2MNK
   return 2.0 * M * N * K;
 }
@@ -329,6 +344,35 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
   return 0;
 }
 
+// Rows [r0, r1) of the predictive product V = L⁻¹K_f* (cal_mean_and_cov KF:121-126; V is
+// never stored): per 128-row tile the column partials Σ_rows w·V and Σ_rows V∘V go to pslab
+// rows [r0/128, r1/128); row r needs L⁻¹ columns ≤ r only (K clipped at tri_off + row).
+// (Forming rows [0, n1) during the factorisation, as FITC does with q, measured 1.3 % slower
+// on C3: profiles/r2_ab_pred_pre.txt.)
+int pred_rows(gps_ctx* ctx, int64_t r0, int64_t r1, const double* w, hipStream_t st) {
+  const int64_t np = ctx->n_pad, ntp = ctx->nt_pad, tiles_m = np / GPS_TILE;
+  GemmParams p = gp0();
+  p.A = ctx->Linv.d() + r0 * np; p.lda = np; p.B = ctx->Ksf.d(); p.ldb = np;
+  p.M = (int)(r1 - r0); p.N = (int)ntp; p.K = (int)r1; p.tri = TRI_K_LE_I; p.tri_off = (int)r0;
+  p.w = w + r0;
+  p.out0 = ctx->pslab.d() + (r0 / GPS_TILE) * ntp;
+  p.out1 = ctx->pslab.d() + (tiles_m + r0 / GPS_TILE) * ntp;
+  p.ld_out = ntp;
+  return gemm(ctx, LAY_N, LAY_T, EPI_COLRED, p, st);
+}
+
+// FITC row norms ‖L⁻¹k_i‖² (K20:222-234 restated): output column tiles [c0, c1) of Knm·L⁻ᵀ
+// (rows [c0, c1) of the triangular L⁻¹, K clipped at the column) into fslab rows [c0/128,
+// c1/128); columns [0, n1) need only the top-level L11⁻¹.
+int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipStream_t st) {
+  const int64_t np = ctx->fn_pad, mp = ctx->m_pad;
+  GemmParams p = gp0();
+  p.A = ctx->Knm.d(); p.lda = mp; p.B = Lx + c0 * mp; p.ldb = mp;
+  p.M = (int)np; p.N = (int)(c1 - c0); p.K = (int)c1; p.tri = TRI_K_LE_J; p.tri_off = (int)c0;
+  p.out0 = ctx->fslab.d() + (c0 / GPS_TILE) * np; p.ld_out = np;
+  return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
+}
+
 // recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
 // W is this level's workspace (n1·n2 doubles); deeper levels on the A22 side get
 // the region after it, so a concurrent GEMM that still reads this level's W never
@@ -341,7 +385,7 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
 // slower end to end, because the side stream's T product already fills the idle slots.
 int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
                   int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
-                  int64_t ldlo) {
+                  int64_t ldlo, bool top = false) {
   hipStream_t s = ctx->stream;
   if (nb == 1) {
     Prof pr(ctx, "potrf_diag128", 2.0 * 128 * 128 * 128 / 3.0, 0);
@@ -387,6 +431,21 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, ts))) return rc;
   }
   if (forked) HIPCHK(hipEventRecord(join, ts));
+  // top level with a pre-pass request: L11⁻¹ is final now, so the product that needs only its
+  // rows (FITC: the q column tiles [0, n1)) runs on aux[0] while rec(A22) — mostly
+  // latency-bound launches at m ≤ 4k — runs
+  if (top && ctx->pre.kind == PRE_FITC_Q && ctx->pre.n1 == n1) {
+    hipStream_t ps = ctx->overlap ? ctx->aux[0] : s;
+    if (ps != s) {
+      hipEvent_t f = sync_event(ctx);
+      ctx->pre.join = sync_event(ctx);
+      if (!f || !ctx->pre.join) return fail(ctx, -2, "hipEventCreate failed");
+      HIPCHK(hipEventRecord(f, s));
+      HIPCHK(hipStreamWaitEvent(ps, f, 0));
+    }
+    if ((rc = fitc_rowsq_cols(ctx, Linv, 0, n1, ps))) return rc;
+    if (ps != s) HIPCHK(hipEventRecord(ctx->pre.join, ps));
+  }
   if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W + (int64_t)n1 * n2, n2b, logdiag + n1, info,
                           base + n1, nreal - n1, Lout ? Lout + (int64_t)n1 * ldlo + n1 : nullptr,
                           ldlo)))
@@ -397,6 +456,10 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     p.A = Li22; p.lda = ldl; p.B = A21; p.ldb = lda; p.C = Li21; p.ldc = ldl;
     p.M = n2; p.N = n1; p.K = n2; p.alpha = -1.0; p.tri = TRI_K_LE_I;
     if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
+  }
+  if (top && ctx->pre.join) {
+    HIPCHK(hipStreamWaitEvent(s, ctx->pre.join, 0));
+    ctx->pre.join = nullptr;
   }
   return 0;
 }
@@ -428,16 +491,22 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
               int nreal, double* Lout) {
   auto eager = [&]() {
     ctx->sync_used = 0;
+    ctx->pre.join = nullptr;
     return potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
-                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad);
+                         static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad, true);
   };
   if (!ctx->graphs || ctx->prof || n_pad <= GPS_TILE) return eager();
+  const bool pre = ctx->pre.kind == PRE_FITC_Q;
   const std::vector<uintptr_t> key = {
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
       (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->gemm_map,
       (uintptr_t)g_tiny_gemm, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
-      (uintptr_t)ctx->ws_side.p};
+      (uintptr_t)ctx->ws_side.p, (uintptr_t)pre,
+      // the pre-pass's operands (only when it is part of the sequence)
+      pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
+      pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
+      pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       g.used = ++ctx->pgraph_clock;
@@ -997,7 +1066,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   DBuf* all[] = {&ctx->info, &ctx->small, &ctx->X, &ctx->y, &ctx->Xt, &ctx->yt, &ctx->A,
                  &ctx->Linv, &ctx->W, &ctx->logdiag, &ctx->beta, &ctx->alpha, &ctx->dinv,
                  &ctx->slab, &ctx->mu_loo, &ctx->var_loo, &ctx->Ksf, &ctx->s1, &ctx->s2,
-                 &ctx->mu, &ctx->var, &ctx->Lout, &ctx->fX, &ctx->fy, &ctx->fXt, &ctx->fyt,
+                 &ctx->mu, &ctx->var, &ctx->Lout, &ctx->pslab, &ctx->fX, &ctx->fy, &ctx->fXt, &ctx->fyt,
                  &ctx->Z, &ctx->Kmm, &ctx->Am, &ctx->Lm, &ctx->Lb, &ctx->ldm, &ctx->ldb,
                  &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
                  &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
@@ -1049,6 +1118,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
+    case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;
     default: return fail(ctx, -1, "unknown option");
   }
 }
@@ -1464,28 +1534,21 @@ int gps_full_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   const int64_t n = ctx->n, np = ctx->n_pad, nt = ctx->nt, ntp = ctx->nt_pad;
   hipStream_t s = ctx->stream;
   const int64_t tiles_m = np / GPS_TILE;
-  HIPCHK(ensure(ctx->Ksf, (size_t)ntp * np * 8));
-  HIPCHK(ensure(ctx->slab, std::max(ctx->slab.cap, (size_t)tiles_m * ntp * 2 * 8)));
   HIPCHK(ensure(ctx->s1, ntp * 8));
   HIPCHK(ensure(ctx->s2, ntp * 8));
   HIPCHK(ensure(ctx->mu, ntp * 8));
   HIPCHK(ensure(ctx->var, ntp * 8));
   int rc;
+  HIPCHK(ensure(ctx->Ksf, (size_t)ntp * np * 8));
+  HIPCHK(ensure(ctx->pslab, (size_t)tiles_m * ntp * 2 * 8));
   if ((rc = gram(ctx, "gram_ksf", ctx->Xt.d(), (int)nt, ctx->X.d(), (int)n, ctx->d, ctx->th, 0.0, 0,
                  0, ctx->Ksf.d(), np, (int)ntp, (int)np)))
     return rc;
-  {
-    GemmParams p = gp0();
-    p.A = ctx->Linv.d(); p.lda = np; p.B = ctx->Ksf.d(); p.ldb = np;
-    p.M = (int)np; p.N = (int)ntp; p.K = (int)np; p.tri = TRI_K_LE_I;
-    p.w = ctx->beta.d(); p.out0 = ctx->slab.d(); p.out1 = ctx->slab.d() + tiles_m * ntp;
-    p.ld_out = ntp;
-    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_COLRED, p))) return rc;
-  }
+  if ((rc = pred_rows(ctx, 0, np, ctx->beta.d(), s))) return rc;
   {
     Prof pr(ctx, "pred_finalize", 0, 0);
-    HIPCHK(launch_slab_sum(ctx->slab.d(), ntp, (int)tiles_m, ntp, nullptr, ctx->s1.d(), s));
-    HIPCHK(launch_slab_sum(ctx->slab.d() + tiles_m * ntp, ntp, (int)tiles_m, ntp, nullptr,
+    HIPCHK(launch_slab_sum(ctx->pslab.d(), ntp, (int)tiles_m, ntp, nullptr, ctx->s1.d(), s));
+    HIPCHK(launch_slab_sum(ctx->pslab.d() + tiles_m * ntp, ntp, (int)tiles_m, ntp, nullptr,
                            ctx->s2.d(), s));
     HIPCHK(launch_pred_finalize(ctx->s1.d(), ctx->s2.d(), (int)nt, ctx->th.sn2 + ctx->th.sf2,
                                 ctx->mu.d(), ctx->var.d(), s));
@@ -1673,21 +1736,23 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                  ctx->Kmm.d(), mp, (int)mp, (int)mp)))
     return rc;
   HIPCHK(hipMemcpyAsync(ctx->Am.p, ctx->Kmm.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
-  if ((rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr)))
-    return rc;
-  HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
-  // --- this shard's rows
+  // this shard's rows of K(X, Z) first: the q column tiles [0, n1) run on aux[0] during Lm's
+  // factorisation (PRE_FITC_Q) as soon as the top-level Lm11⁻¹ is final
   if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
                  ctx->Knm.d(), mp, (int)np, (int)mp)))
     return rc;
-  {  // q_i = ‖Lm⁻¹ k_i‖²
-    GemmParams p = gp0();
-    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lm.d(); p.ldb = mp;
-    p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
-    p.out0 = ctx->fslab.d(); p.ld_out = np;
-    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p))) return rc;
-    HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->q.d(), s));
-  }
+  const bool preq = ctx->pred_pre && mp > GPS_TILE;
+  const int64_t qn1 = preq ? (mp / GPS_TILE / 2) * GPS_TILE : 0;
+  ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
+  ctx->pre.n1 = qn1;
+  ctx->pre.L = ctx->Lm.d();
+  rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr);
+  ctx->pre.kind = PRE_NONE;
+  if (rc) return rc;
+  HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
+  // q_i = ‖Lm⁻¹ k_i‖² (the remaining column tiles)
+  if ((rc = fitc_rowsq_cols(ctx, ctx->Lm.d(), qn1, mp, s))) return rc;
+  HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->q.d(), s));
   {
     Prof pr(ctx, "fitc_lambda", 0, 0);
     HIPCHK(launch_fitc_lambda(ctx->q.d(), ctx->fy.d(), (int)n, (int)np, th.sf2, th.sn2,

@@ -58,7 +58,9 @@ struct GemmParams {
   int lower_out;             // enumerate only tiles with tj <= ti
   int ksplit;                // number of K slices (grid.y)
   int tri;
-  const int* kr;             // TRI_KR_J: per 16-column group [k begin, k end) (multiples of 16)
+  int tri_off;               // global index of output row / column 0 for the tri clipping (a
+                             // row or column block of a larger triangular product)
+  const int* kr;            // TRI_KR_J: per 16-column group [k begin, k end) (multiples of 16)
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
                              // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto

@@ -152,10 +152,10 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
 
   int kb = 0, ke = p.K;
   switch (p.tri) {
-    case TRI_K_LE_I: ke = min(ke, row0 + TILE); break;
-    case TRI_K_LE_J: ke = min(ke, col0 + TILE); break;
-    case TRI_K_GE_J: kb = col0; break;
-    case TRI_K_GE_I: kb = row0; break;
+    case TRI_K_LE_I: ke = min(ke, p.tri_off + row0 + TILE); break;
+    case TRI_K_LE_J: ke = min(ke, p.tri_off + col0 + TILE); break;
+    case TRI_K_GE_J: kb = p.tri_off + col0; break;
+    case TRI_K_GE_I: kb = p.tri_off + row0; break;
     case TRI_KR_J:
       kb = p.kr[2 * (col0 / 16)];
       ke = p.kr[2 * ((col0 + TILE) / 16 - 1) + 1];
@@ -393,10 +393,10 @@ __global__ __launch_bounds__(256) void gemm_f64_small_kernel(GemmParams p) {
   const int row0 = ti * TE, col0 = tj * TE;
   int kb = 0, ke = p.K;
   switch (p.tri) {
-    case TRI_K_LE_I: ke = min(ke, row0 + TE); break;
-    case TRI_K_LE_J: ke = min(ke, col0 + TE); break;
-    case TRI_K_GE_J: kb = col0; break;
-    case TRI_K_GE_I: kb = row0; break;
+    case TRI_K_LE_I: ke = min(ke, p.tri_off + row0 + TE); break;
+    case TRI_K_LE_J: ke = min(ke, p.tri_off + col0 + TE); break;
+    case TRI_K_GE_J: kb = p.tri_off + col0; break;
+    case TRI_K_GE_I: kb = p.tri_off + row0; break;
     case TRI_KR_J:
       kb = p.kr[2 * (col0 / 16)];
       ke = p.kr[2 * ((col0 + TE) / 16 - 1) + 1];

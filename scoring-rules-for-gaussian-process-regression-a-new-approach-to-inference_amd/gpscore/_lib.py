@@ -19,6 +19,7 @@ GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
 GPS_OPT_GRAPH = 10
+GPS_OPT_PRED_PRE = 11
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
 GPS_SURF_LOGS_ADD_NOISE = 1
@@ -186,6 +187,11 @@ class Context:
         """Replay the recursive factorisation from a captured hipGraph (default) or launch
         it eagerly."""
         self.call("gps_ctx_set_option", GPS_OPT_GRAPH, 1 if on else 0)
+
+    def set_pred_pre(self, on=True):
+        """FITC: form the q_i = ||Lm^-1 k_i||^2 columns that need only the top-level Lm11^-1
+        during Lm's factorisation (default), or the whole pass after it."""
+        self.call("gps_ctx_set_option", GPS_OPT_PRED_PRE, 1 if on else 0)
 
     def synchronize(self):
         self.call("gps_ctx_synchronize")

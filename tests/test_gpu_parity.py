@@ -284,6 +284,32 @@ def test_stream_schedules_agree(gp, gpu_ctx):
     assert nrel(r0.mu_loo, f["loo_mu"]) < 1e-9 and abs(r0.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
+def test_fitc_q_prepass_matches(gp, gpu_ctx):
+    """GPS_OPT_PRED_PRE for FITC: the q_i = ‖Lm⁻¹k_i‖² column tiles [0, n1) run on aux[0]
+    during Lm's factorisation, the rest after it — same tiles and K ranges as one launch, so
+    fit, LOO vectors and predictives agree to 1e-14 with the option off (and with the oracle)."""
+    rng = np.random.default_rng(13)
+    n, nt, m, d = 9000, 700, 1100, 8
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
+    Z = X[rng.choice(n, m, replace=False)]
+    y, yt = np.sin(X.sum(1)), np.sin(Xt.sum(1))
+    th = (0.0, np.log(1.5) * np.ones(d), np.log(0.05))
+    runs = []
+    try:
+        for pre in (False, True):
+            gpu_ctx.set_pred_pre(pre)
+            runs.append(_unit(gp, X, y, Xt, yt, th, Z=Z))
+    finally:
+        gpu_ctx.set_pred_pre(True)
+    a, b = runs
+    for k in UNIT_VECS:
+        assert nrel(b[k], a[k]) < 1e-14, k
+    for k in UNIT_SCAL:
+        assert abs(float(b[k]) - float(a[k])) <= 1e-13 * max(1.0, abs(float(a[k]))), k
+    ref = O.fast_fitc(X, y, Xt, yt, Z, *th)
+    assert nrel(b["pred_mu"], ref["pred_mu"]) < 1e-6 and nrel(b["loo_mu"], ref["loo_mu"]) < 1e-6
+
+
 def test_new_input_dimension_voids_test_set(gpu_ctx):
     """set_data with another input dimension drops the resident test set (and, for FITC, the
     inducing points) at the C-ABI: predict / fit then report what is missing instead of
