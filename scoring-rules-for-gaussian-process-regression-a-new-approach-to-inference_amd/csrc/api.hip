@@ -105,10 +105,9 @@ struct gps_ctx {
   struct PotrfGraph {                  // one captured potrf_inv launch sequence
     std::vector<uintptr_t> key;
     hipGraphExec_t exec = nullptr;
-    uint64_t used = 0;
   };
-  std::vector<PotrfGraph> pgraphs;     // small LRU keyed by buffers, sizes, streams, options
-  uint64_t pgraph_clock = 0;
+  std::vector<PotrfGraph> pgraphs;     // keyed by buffers, sizes, streams, options; kept until
+                                       // the context is destroyed (potrf_inv: kMaxGraphs)
   std::string err;
   // profiling
   int prof = 0;  // 1: per-tag timing, 2: per-shape tags
@@ -487,6 +486,8 @@ int reset_info(gps_ctx* ctx) {
 // became the bound.  With GPS_OPT_GRAPH (default) the whole sequence is captured once per
 // (buffers, sizes, streams, options) into a hipGraph and replayed with one launch; the
 // eager path remains for profiling (per-launch events) and as the option's off state.
+constexpr size_t kMaxGraphs = 256;
+
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
   auto eager = [&]() {
@@ -509,10 +510,15 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
-      g.used = ++ctx->pgraph_clock;
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
       return 0;
     }
+  // Graphs are never destroyed while the context lives: with the HIP runtime that PyTorch
+  // bundles (ROCm 7.0, which serves this library whenever torch is imported first), destroying
+  // a replayed graph exec — even after a device synchronize — made the next capture / replay
+  // segfault on the host (GPU suite, FITC gradient after ~60 cached shapes; a 64-entry cache or
+  // eager launches did not crash).  Past kMaxGraphs shapes the factorisation runs eagerly.
+  if (ctx->pgraphs.size() >= kMaxGraphs) return eager();
   // capture: everything the recursion allocates must exist beforehand (no allocation
   // inside a capture): the split-K workspaces and the fork/join event pool
   HIPCHK(ensure(ctx->ws_main, (size_t)kSplitWsDoubles * 8));
@@ -538,13 +544,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   HIPCHK(ei);
-  if (ctx->pgraphs.size() >= 8) {  // evict the least recently used
-    auto lru = std::min_element(ctx->pgraphs.begin(), ctx->pgraphs.end(),
-                                [](const auto& a, const auto& b) { return a.used < b.used; });
-    (void)hipGraphExecDestroy(lru->exec);
-    ctx->pgraphs.erase(lru);
-  }
-  ctx->pgraphs.push_back({key, exec, ++ctx->pgraph_clock});
+  ctx->pgraphs.push_back({key, exec});
   HIPCHK(hipGraphLaunch(exec, ctx->stream));
   return 0;
 }

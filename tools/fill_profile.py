@@ -2,7 +2,8 @@
 workgroups of the running kernels (summed over queues) against the 512 slots of two
 workgroups per CU.  Reports the fill-weighted time, the time spent below half fill and
 the kernels running then — where the latency-bound chain leaves the chip idle.
-Usage: python tools/fill_profile.py <run_kernel_trace.csv> <first-kernel-substring> [unit]"""
+Usage: python tools/fill_profile.py <run_kernel_trace.csv> <first-kernel-substring> [unit] [stride]
+(stride: marker kernels per unit, e.g. 2 Gram launches per full-GP unit, 3 per FITC unit)"""
 import collections
 import csv
 import sys
@@ -19,8 +20,9 @@ for r in csv.DictReader(open(sys.argv[1])):
 rows.sort()
 marks = [i for i, k in enumerate(rows) if sys.argv[2] in k[2]]
 u = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-a = marks[u]
-b = marks[u + 1] if u + 1 < len(marks) else len(rows)
+st = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+a = marks[u * st]
+b = marks[(u + 1) * st] if (u + 1) * st < len(marks) else len(rows)
 unit = rows[a:b]
 t0 = unit[0][0]
 t1 = max(e for _, e, _, _ in unit)
