@@ -63,7 +63,8 @@ struct GemmParams {
   const int* kr;            // TRI_KR_J: per 16-column group [k begin, k end) (multiples of 16)
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
-                             // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto
+                             // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto,
+                             // 5 XCD-banded 8×8 patches (auto for EPI_ROWSQ), 6 auto without 5
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)

@@ -87,6 +87,23 @@ __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int
     tj = p.tri == TRI_K_LE_J ? p.tiles_n - 1 - cj : cj;
     return ti < p.tiles_m && cj < p.tiles_n;
   }
+  if (p.map_mode == 5) {
+    // XCD-banded 8×8 patches (triangular operands, A/B): as map 3, XCD x owns a band of the
+    // index that does not carry the triangular work, but its resident tiles form 8 (band) × 8
+    // (work index) patches, the work index walked heaviest-first patch by patch, so an 8×8
+    // group of tiles with neighbouring K ranges shares both operand panels in its L2.
+    const int x = t & 7, i = t >> 3;
+    const bool wi = p.tri == TRI_K_LE_I || p.tri == TRI_K_GE_I;  // work follows ti
+    const int nb = wi ? p.tiles_n : p.tiles_m, nw = wi ? p.tiles_m : p.tiles_n;
+    const int bb = (nb + 7) >> 3, per = ((bb + 7) >> 3) * 64;
+    const int wg = i / per, rem = i - wg * per, w = rem & 63;
+    const int bi = x * bb + (rem >> 6) * 8 + (w & 7), wk = wg * 8 + (w >> 3);
+    if (bi >= min(nb, x * bb + bb) || wk >= nw) return false;
+    const int widx = (p.tri == TRI_K_LE_I || p.tri == TRI_K_LE_J) ? nw - 1 - wk : wk;
+    ti = wi ? widx : bi;
+    tj = wi ? bi : widx;
+    return true;
+  }
   const int per_group = GROUP_M * p.tiles_n;
   const int g = t / per_group;
   const int first = g * GROUP_M;
@@ -625,9 +642,20 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   q.tiles_n = q.N / tile;
   int tiles = (int)tiles_for(q, tile);
   // triangular operands default to the XCD-banded heaviest-first order (map 3):
-  // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build
-  if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out) q.map_mode = 3;
+  // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build; the
+  // FITC row norms (EPI_ROWSQ) to its 8×8-patch form (map 5): C5 173.6 vs 176.6 ms, while the
+  // patch order on the factorisation / predictive TRMMs cost C3 27 % (profiles/r2_map5_ab.txt)
+  const bool rowsq_patch = q.map_mode != 6;  // 6: the automatic order without it (A/B runs)
+  if (q.map_mode == 6) q.map_mode = 0;
+  if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out)
+    q.map_mode = epi == EPI_ROWSQ && rowsq_patch ? 5 : 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
+  if (q.map_mode == 5 && (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J)) q.map_mode = 0;
+  if (q.map_mode == 5) {  // 8 XCDs × ceil(work / 8) groups × the band's 8-wide groups × 64
+    const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;
+    const int nb = wi ? q.tiles_n : q.tiles_m, nw = wi ? q.tiles_m : q.tiles_n;
+    tiles = 8 * ((nw + 7) / 8) * (((nb + 7) / 8 + 7) / 8) * 64;
+  }
   if (q.map_mode == 3) {
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
