@@ -262,7 +262,7 @@ const char* gemm_tag(int al, int bl, int epi, const GemmParams& p) {
   (void)al;
   (void)bl;
   if (epi == EPI_COLRED) return "gemm_trmm_colred";
-  if (epi == EPI_ROWSQ) return "gemm_rowsq";
+  if (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) return "gemm_rowsq";
   const int64_t tiles = (int64_t)(p.M / GPS_TILE) * (p.N / GPS_TILE) / (p.lower_out ? 2 : 1);
   const int cls = tiles < 16 ? 0 : (tiles < 256 ? 1 : 2);
   static const char* syrk[3] = {"gemm_syrk_s", "gemm_syrk_m", "gemm_syrk_l"};
@@ -1786,17 +1786,17 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                          nullptr, ctx->fslab.d(), s));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
-  {  // r_i = ‖Lb⁻¹ k_i‖²
+  {  // r_i = ‖Lb⁻¹ k_i‖², and g = Knm c from the same pass over Knm (its last column tile)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp;
     p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
     p.out0 = ctx->fslab.d(); p.ld_out = np;
-    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p))) return rc;
+    p.w = ctx->c.d(); p.out1 = ctx->g.d();
+    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ_DOT, p))) return rc;
     HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->r.d(), s));
   }
   {
-    Prof pr(ctx, "fitc_loo", 0, 8.0 * np * mp);
-    HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, ctx->c.d(), ctx->g.d(), (int)np, (int)mp, s));
+    Prof pr(ctx, "fitc_loo", 0, 0);
     HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n,
                            ctx->fmu_loo.d(), ctx->fvar_loo.d(), scal + 2, s));
   }

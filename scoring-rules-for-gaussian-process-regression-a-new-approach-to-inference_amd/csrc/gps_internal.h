@@ -43,7 +43,8 @@ enum Tri {
   TRI_KR_J = 5,    // k in [kr[2g], kr[2g'+1]) over the 16-column groups g..g' of the tile
                    // (B block-diagonal with unaligned blocks: block-LOO gradients)
 };
-enum Epi { EPI_STORE = 0, EPI_ROWSQ = 1, EPI_COLRED = 2 };
+enum Epi { EPI_STORE = 0, EPI_ROWSQ = 1, EPI_COLRED = 2, EPI_ROWSQ_DOT = 3 };
+// EPI_ROWSQ_DOT: EPI_ROWSQ plus, in the last column tile (the full K range), out1[row] = A[row,:]·w
 
 struct GemmParams {
   const double* A; int64_t lda;

@@ -280,6 +280,21 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     }
   };
 
+  // EPI_ROWSQ_DOT: the last column tile spans the full K range, so its A rows also give
+  // A[row,:]·w — threads 0..TILE-1 take one row each from the slice image in LDS (w read
+  // wave-uniform), which spares the caller a separate pass over A (FITC g = Knm c)
+  const bool rdot = EPI == EPI_ROWSQ_DOT && tj == p.tiles_n - 1 && kb == 0;
+  double dacc = 0.0;
+  auto row_dot = [&](int buf, int k0) {
+    if constexpr (EPI == EPI_ROWSQ_DOT) {
+      if (rdot && tid < TILE) {
+        const double* As = smem + buf * STAGE;
+#pragma unroll
+        for (int k = 0; k < BK; ++k) dacc = fma(As[rowoff(k) + tid], p.w[k0 + k], dacc);
+      }
+    }
+  };
+
   if (nk > 0) {
     load_tile(kb);
     store_tile(0);
@@ -289,10 +304,15 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     for (int it = 0; it < nk - 1; ++it) {
       load_tile(kb + (it + 1) * BK);
       compute(it & 1);
+      row_dot(it & 1, kb + it * BK);
       store_tile((it + 1) & 1);
       __syncthreads();
     }
     compute((nk - 1) & 1);
+    row_dot((nk - 1) & 1, kb + (nk - 1) * BK);
+  }
+  if constexpr (EPI == EPI_ROWSQ_DOT) {
+    if (rdot && tid < TILE) p.out1[row0 + tid] = dacc;
   }
 
   const int lrow = lane >> 4, lcol = lane & 15;
@@ -311,7 +331,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
           crow[ni * 16] = v;
         }
       }
-  } else if constexpr (EPI == EPI_ROWSQ) {
+  } else if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
     // out0[tj][row] = sum over this tile's columns of (alpha*acc)^2
     double* red = smem;  // [2 (wc)][TILE rows]
     __syncthreads();
@@ -648,7 +668,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   const bool rowsq_patch = q.map_mode != 6;  // 6: the automatic order without it (A/B runs)
   if (q.map_mode == 6) q.map_mode = 0;
   if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out)
-    q.map_mode = epi == EPI_ROWSQ && rowsq_patch ? 5 : 3;
+    q.map_mode = (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) && rowsq_patch ? 5 : 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
   if (q.map_mode == 5 && (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J)) q.map_mode = 0;
   if (q.map_mode == 5) {  // 8 XCDs × ceil(work / 8) groups × the band's 8-wide groups × 64
@@ -673,6 +693,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE, 128)
   GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE, 128)
   GPS_GEMM_CASE(LAY_N, LAY_T, EPI_ROWSQ, 128)
+  GPS_GEMM_CASE(LAY_N, LAY_T, EPI_ROWSQ_DOT, 128)
   GPS_GEMM_CASE(LAY_N, LAY_T, EPI_COLRED, 128)
   GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE, 64)
   GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE, 64)
