@@ -88,7 +88,7 @@ __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int
     return ti < p.tiles_m && cj < p.tiles_n;
   }
   if (p.map_mode == 5) {
-    // XCD-banded 8×8 patches (triangular operands, A/B): as map 3, XCD x owns a band of the
+    // XCD-banded 8×8 patches (the automatic order of the FITC row norms): as map 3, XCD x owns a band of the
     // index that does not carry the triangular work, but its resident tiles form 8 (band) × 8
     // (work index) patches, the work index walked heaviest-first patch by patch, so an 8×8
     // group of tiles with neighbouring K ranges shares both operand panels in its L2.
@@ -619,6 +619,10 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   if ((p.lda & 1) || (p.ldb & 1) || (p.ldc & 1)) return hipErrorInvalidValue;
   if (p.lower_out && p.M != p.N) return hipErrorInvalidValue;
   if (p.ksplit < 1) p.ksplit = 1;
+  // the row dot comes from the last column tile, which must span the whole K range
+  if (epi == EPI_ROWSQ_DOT &&
+      (!p.w || !p.out1 || p.tri != TRI_K_LE_J || p.tri_off != 0 || p.K != p.N || p.ksplit != 1))
+    return hipErrorInvalidValue;
   const GemmPlan plan = gemm_plan(epi, p, p.ws ? p.ws_cap : 0);
   const int tile = plan.tile;
   if (tile == 16 || tile == 32) {  // small kernel: tile = block edge, ksplit = waves per block
@@ -663,7 +667,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   int tiles = (int)tiles_for(q, tile);
   // triangular operands default to the XCD-banded heaviest-first order (map 3):
   // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build; the
-  // FITC row norms (EPI_ROWSQ) to its 8×8-patch form (map 5): C5 173.6 vs 176.6 ms, while the
+  // FITC row norms (EPI_ROWSQ) to its 8×8-patch form (map 5): C5 174.0 vs 181.5 ms, while the
   // patch order on the factorisation / predictive TRMMs cost C3 27 % (profiles/r2_map5_ab.txt)
   const bool rowsq_patch = q.map_mode != 6;  // 6: the automatic order without it (A/B runs)
   if (q.map_mode == 6) q.map_mode = 0;
