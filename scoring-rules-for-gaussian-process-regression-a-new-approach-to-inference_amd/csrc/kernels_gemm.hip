@@ -88,8 +88,8 @@ __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int
     return ti < p.tiles_m && cj < p.tiles_n;
   }
   if (p.map_mode == 5) {
-    // XCD-banded 8×8 patches (the automatic order of the FITC row norms): as map 3, XCD x owns a band of the
-    // index that does not carry the triangular work, but its resident tiles form 8 (band) × 8
+    // XCD-banded 8×8 patches (the automatic order of the FITC row norms): as map 3, XCD x owns
+    // a band of the index that does not carry the triangular work, but its resident tiles form 8 (band) × 8
     // (work index) patches, the work index walked heaviest-first patch by patch, so an 8×8
     // group of tiles with neighbouring K ranges shares both operand panels in its L2.
     const int x = t & 7, i = t >> 3;
