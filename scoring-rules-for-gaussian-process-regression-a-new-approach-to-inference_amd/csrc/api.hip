@@ -1633,6 +1633,10 @@ int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* ds
     ks = k;
     if (wg >= 1024 && (double)wg / (512.0 * rounds) >= 0.95) break;
   }
+  // and slices of at most ~8k rows: at n = 200k (C5) 24 slices ran 1 % faster than the 12 the
+  // fill rule gives (more workgroups share each slice's rows through the Infinity Cache), at
+  // n = 40k (C4) more slices than the fill rule's 11 were slower (profiles/r2_syrk_ks_ab.txt)
+  ks = (int)std::max<int64_t>(ks, std::min<int64_t>(32, (np + 8191) / 8192));
   HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
   GemmParams p = gp0();
   p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
