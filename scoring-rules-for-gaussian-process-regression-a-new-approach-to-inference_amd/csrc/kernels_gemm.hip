@@ -602,7 +602,9 @@ GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap) {
     if (p.lower_out ? (p.M <= 640 && p.K <= 640) : (mn <= 1280 * 1280 && (p.tri || p.K <= 640)))
       return {32, small_wpt(p.K)};
   }
-  if (tiles_for(p, 128) >= 1024) return {128, 1};
+  // 128-tiles from 512 of them (the 5k-level trailing SYRK, 780 lower tiles, left the 64-tile
+  // path: C3 -0.7 %; 256 was slower — the 2.5k-level TRMMs want 64-tiles: profiles/r2_t128_ab.txt)
+  if (tiles_for(p, 128) >= 512) return {128, 1};
   const int64_t t64 = tiles_for(p, 64);
   const int64_t target = p.lower_out ? 2048 : 1024;
   int ks = 1;
