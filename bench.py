@@ -220,10 +220,20 @@ def _oracle():
     return O, RT
 
 
+def host_cores():
+    """The host threads this process may use and how that was decided: the CPU affinity mask
+    (os.sched_getaffinity), capped by OMP_NUM_THREADS when the box sets it (the lease's share
+    on a shared host; os.cpu_count() reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    used = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return used, {"threads_used": used, "sched_getaffinity": aff, "os_cpu_count": os.cpu_count(),
+                  "OMP_NUM_THREADS": omp}
+
+
 def _torch_threads():
-    """All host threads the box gives this process (OMP_NUM_THREADS is set there)."""
     import torch
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cores, _ = host_cores()
     torch.set_num_threads(cores)
     return cores
 
@@ -234,19 +244,32 @@ def cpu_baseline(config="C3"):
     chol_solve(I, A), full n*×n* covariance; KF:239-245, 329-334, 365-391) — timed on ONE
     full C3 unit on the box's host threads (BASELINE.md:48-57).  Also returns its outputs,
     which the parity record compares with the GPU unit."""
-    _, RT = _oracle()
+    O, RT = _oracle()
     cores = _torch_threads()
+    _, cinfo = host_cores()
     c = CONFIGS[config]
     X, y, Xt, yt, _, th = synth(c["n"], c["d"], c["nt"], c["seed"])
     t0 = time.perf_counter()
     ref = RT.ref_full(X, y, Xt, yt, *th)
     t = time.perf_counter() - t0
+    # BASELINE.md:53's second CPU figure: the numpy/LAPACK potrf + trsm restatement (the GPU's
+    # algorithm, oracle.fast_full) on the same unit and the same number of BLAS threads
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=cores):
+        t0 = time.perf_counter()
+        O.fast_full(X, y, Xt, yt, *th)
+        t_fast = time.perf_counter() - t0
     info = RT.host_info()
+    info.update(cinfo)
     return {"value": 1.0 / t, "unit": f"fit+predict+score units/s ({config})",
             "cores": cores, "kind": "port", "host": info,
             "sample": f"torch-CPU fp64 ref-mirror of the reference op sequence on the full C3 "
                       f"workload {config} n={c['n']} d={c['d']} n*={c['nt']}, one unit: {t:.1f} s "
-                      f"({info['cpu_model']}, {cores} threads, BLAS {info['blas']})"}, ref
+                      f"({info['cpu_model']}, {cores} threads, BLAS {info['blas']})",
+            "fast_cpu_s": t_fast,
+            "fast_cpu_note": "oracle.fast_full: numpy/LAPACK potrf + L^-1 products on the same unit "
+                             f"and {cores} BLAS threads (the GPU's algorithm, not the reference's "
+                             "op sequence)"}, ref
 
 
 PARITY_VECS = ("loo_mu", "loo_var", "pred_mu", "pred_var")

@@ -89,6 +89,16 @@ enum {
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
+/* Context statistics: out[GPS_STAT_GRAPHS] factorisation graphs cached (one per distinct
+ * (buffers, size, streams, options); each holds its instantiated launch sequence, ~1-3 MB of
+ * host memory and a few KB of device memory, until the context is destroyed),
+ * out[GPS_STAT_GRAPH_CAP] the cache's capacity, out[GPS_STAT_GRAPH_OVERFLOW] factorisations
+ * that ran as eager launches because the cache was full (same results, more host time),
+ * out[GPS_STAT_DEVICE_BYTES] device memory held by the context's buffers. */
+enum { GPS_STAT_GRAPHS = 0, GPS_STAT_GRAPH_CAP = 1, GPS_STAT_GRAPH_OVERFLOW = 2,
+       GPS_STAT_DEVICE_BYTES = 3, GPS_N_STATS = 4 };
+int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
+
 /* on: 0 off, 1 per-kernel-class tags, 2 GEMM tags also carry layout/shape/tri/split-K/lda */
 int gps_prof_enable(gps_ctx* ctx, int on);
 /* Synchronises, then writes a JSON object {tag: {count, ms, flop, bytes}} and clears. */
@@ -217,7 +227,10 @@ int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]);
  * own host thread, e.g. several shards on one GPU) that pass the same `group` key meet at every
  * all-reduce of the FITC path, where their partials are summed on the host in rank order.
  * Same call sites and element counts as the RCCL path; used to test the row-sharded FITC
- * bookkeeping without a multi-GPU node (a rank that waits > 300 s returns an error). */
+ * bookkeeping without a multi-GPU node.  A rank that waits > 60 s, or a member that leaves,
+ * aborts the group: every member's current and later all-reduces then fail (call
+ * gps_comm_init_local again, which joins a fresh group under the same key).  Two live
+ * contexts may not hold the same rank of one group. */
 int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group);
 /* Leaves either communicator. */
 int gps_comm_destroy(gps_ctx* ctx);

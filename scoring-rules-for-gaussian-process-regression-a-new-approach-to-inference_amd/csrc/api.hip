@@ -72,6 +72,7 @@ struct LocalGroup {
   bool aborted = false;  // a member left (comm destroy / context destroy): waits fail at once
   std::vector<std::vector<double>> in;
   std::vector<double> sum;
+  std::vector<char> taken;  // ranks held by a live context (a second context may not join as one)
 };
 std::mutex g_groups_mu;
 std::map<long long, std::weak_ptr<LocalGroup>> g_groups;
@@ -108,6 +109,7 @@ struct gps_ctx {
   };
   std::vector<PotrfGraph> pgraphs;     // keyed by buffers, sizes, streams, options; kept until
                                        // the context is destroyed (potrf_inv: kMaxGraphs)
+  int64_t graph_overflow = 0;          // factorisations run eagerly because the cache was full
   std::string err;
   // profiling
   int prof = 0;  // 1: per-tag timing, 2: per-shape tags
@@ -518,7 +520,10 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   // a replayed graph exec — even after a device synchronize — made the next capture / replay
   // segfault on the host (GPU suite, FITC gradient after ~60 cached shapes; a 64-entry cache or
   // eager launches did not crash).  Past kMaxGraphs shapes the factorisation runs eagerly.
-  if (ctx->pgraphs.size() >= kMaxGraphs) return eager();
+  if (ctx->pgraphs.size() >= kMaxGraphs) {
+    ++ctx->graph_overflow;
+    return eager();
+  }
   // capture: everything the recursion allocates must exist beforehand (no allocation
   // inside a capture): the split-K workspaces and the fork/join event pool
   HIPCHK(ensure(ctx->ws_main, (size_t)kSplitWsDoubles * 8));
@@ -611,6 +616,7 @@ void leave_local_group(gps_ctx* ctx) {
   {
     std::lock_guard<std::mutex> lk(ctx->lgroup->mu);
     ctx->lgroup->aborted = true;
+    ctx->lgroup->taken[ctx->rank] = 0;
   }
   ctx->lgroup->cv.notify_all();
   ctx->lgroup.reset();
@@ -654,9 +660,12 @@ int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
       G.cv.notify_all();
     } else if (!G.cv.wait_for(lk, std::chrono::seconds(60),
                               [&] { return G.gen != my || G.aborted; })) {
-      return fail(ctx, -3, "local all-reduce: timed out waiting for the other ranks");
+      // a timed-out rank aborts the group, so every member (including a late arriver, which
+      // would otherwise complete this generation with a rank that has left) fails the same way
+      G.aborted = true;
+      G.cv.notify_all();
+      return fail(ctx, -3, "local all-reduce: timed out waiting for the other ranks (group aborted)");
     } else if (G.gen == my) {
-      --G.arrived;
       return fail(ctx, -3, "local all-reduce: another rank left the group");
     }
     out = G.sum;
@@ -1024,6 +1033,24 @@ int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const doub
 }  // namespace
 
 // =============================================================================
+// every device buffer a context owns (destroy, gps_ctx_stats)
+static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
+  return {&ctx->info, &ctx->small, &ctx->X, &ctx->y, &ctx->Xt, &ctx->yt, &ctx->A,
+                 &ctx->Linv, &ctx->W, &ctx->logdiag, &ctx->beta, &ctx->alpha, &ctx->dinv,
+                 &ctx->slab, &ctx->mu_loo, &ctx->var_loo, &ctx->Ksf, &ctx->s1, &ctx->s2,
+                 &ctx->mu, &ctx->var, &ctx->Lout, &ctx->pslab, &ctx->fX, &ctx->fy, &ctx->fXt, &ctx->fyt,
+                 &ctx->Z, &ctx->Kmm, &ctx->Am, &ctx->Lm, &ctx->Lb, &ctx->ldm, &ctx->ldb,
+                 &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
+                 &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
+                 &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->fslab_pre, &ctx->t0,
+                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_aux[0], &ctx->ws_aux[1],
+                 &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
+                 &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
+                 &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
+                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW};
+}
+
 extern "C" {
 
 int gps_version(void) { return 100; }
@@ -1063,21 +1090,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   (void)hipDeviceSynchronize();
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   leave_local_group(ctx);
-  DBuf* all[] = {&ctx->info, &ctx->small, &ctx->X, &ctx->y, &ctx->Xt, &ctx->yt, &ctx->A,
-                 &ctx->Linv, &ctx->W, &ctx->logdiag, &ctx->beta, &ctx->alpha, &ctx->dinv,
-                 &ctx->slab, &ctx->mu_loo, &ctx->var_loo, &ctx->Ksf, &ctx->s1, &ctx->s2,
-                 &ctx->mu, &ctx->var, &ctx->Lout, &ctx->pslab, &ctx->fX, &ctx->fy, &ctx->fXt, &ctx->fyt,
-                 &ctx->Z, &ctx->Kmm, &ctx->Am, &ctx->Lm, &ctx->Lb, &ctx->ldm, &ctx->ldb,
-                 &ctx->Knm, &ctx->q, &ctx->lam, &ctx->ilam, &ctx->ys, &ctx->slabB, &ctx->red,
-                 &ctx->c, &ctx->tvec, &ctx->r, &ctx->g, &ctx->fmu_loo, &ctx->fvar_loo,
-                 &ctx->Ksm, &ctx->qm, &ctx->qb, &ctx->fmu, &ctx->fvar, &ctx->fslab, &ctx->fslab_pre, &ctx->t0,
-                 &ctx->t1, &ctx->t2, &ctx->t3, &ctx->t4, &ctx->ws_main, &ctx->ws_side, &ctx->ws_aux[0], &ctx->ws_aux[1],
-                 &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
-                 &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
-                 &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
-                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW};
-  for (DBuf* b : all) release(*b);
+  for (DBuf* b : ctx_buffers(ctx)) release(*b);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join})
@@ -1128,6 +1141,18 @@ void* gps_ctx_stream(gps_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; 
 int gps_ctx_synchronize(gps_ctx* ctx) {
   if (int rc = bind(ctx)) return rc;
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(out != nullptr, "out is NULL");
+  size_t bytes = 0;
+  for (DBuf* b : ctx_buffers(ctx)) bytes += b->cap;
+  out[GPS_STAT_GRAPHS] = (int64_t)ctx->pgraphs.size();
+  out[GPS_STAT_GRAPH_CAP] = (int64_t)kMaxGraphs;
+  out[GPS_STAT_GRAPH_OVERFLOW] = ctx->graph_overflow;
+  out[GPS_STAT_DEVICE_BYTES] = (int64_t)bytes;
   return 0;
 }
 
@@ -2559,13 +2584,24 @@ int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
   leave_local_group(ctx);
   std::lock_guard<std::mutex> lk(g_groups_mu);
   std::shared_ptr<LocalGroup> G = g_groups[group].lock();
-  if (!G) {
+  bool dead = false;
+  if (G) {
+    std::lock_guard<std::mutex> gl(G->mu);
+    dead = G->aborted;
+  }
+  if (!G || dead) {  // an aborted group is never rejoined: the key gets a fresh group
     G = std::make_shared<LocalGroup>();
     G->n = nranks;
     G->in.resize(nranks);
+    G->taken.assign(nranks, 0);
     g_groups[group] = G;
   }
   ARGCHK(G->n == nranks, "local group: nranks differs from the group's");
+  {
+    std::lock_guard<std::mutex> gl(G->mu);
+    ARGCHK(!G->taken[rank], "local group: another live context already holds this rank");
+    G->taken[rank] = 1;
+  }
   ctx->lgroup = G;
   ctx->nranks = nranks;
   ctx->rank = rank;

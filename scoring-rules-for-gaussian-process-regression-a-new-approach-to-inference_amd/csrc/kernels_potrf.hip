@@ -84,7 +84,7 @@ __device__ __forceinline__ void tile_update2(double* S, int d0, int a0, int d1, 
 // pivot wave: factor panel p held in P (rows l + 64 s), diagonal tile in row slot DS; LO:
 // slot 0 holds panel rows
 template <int DS, bool LO>
-__device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane, double* M) {
+__device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane) {
   const int J0 = 16 * p;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
@@ -101,22 +101,13 @@ __device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane
       const double v = P[s][j] * rs;
       P[s][j] = R > J ? v : (R == J ? ljj : 0.0);
     }
-    double* Mj = M + 16 * (j & 1);  // double-buffered: a lagging read never sees column j+1
-    {
-      const int R = lane + 64 * DS;
-      if (R > J && R < J0 + 16) Mj[R - J0] = P[DS][j];
-    }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
     double m1 = 0.0;
     if (j < 15) m1 = rl(P[DS][j], (J + 1) & 63);
 #pragma unroll
     for (int c = j + 1; c < 16; ++c) {
-#ifdef GPS_V4_PIVOT_LDS
-      const double m = c == j + 1 ? m1 : Mj[c];
-#else
       const double m = c == j + 1 ? m1 : rl(P[DS][j], (J0 + c) & 63);
-#endif
 #pragma unroll
       for (int s = LO ? 0 : 1; s < 2; ++s) P[s][c] = fma(-P[s][j], m, P[s][c]);
     }
@@ -155,15 +146,6 @@ __device__ __forceinline__ void invert_diag(double* S, double* DG, int p, int la
   }
 }
 
-#ifdef GPS_V4_STAMPS
-__device__ long long g_v4_stamps[4][40];  // [wave][event]: tools/diag_bench.cpp timing build only
-#define V4_STAMP(ev) do { if (lane == 0) g_v4_stamps[wave][ev] = __builtin_amdgcn_s_memtime(); } while (0)
-__device__ long long g_v4_pstamps[8][3];  // wave 0 per panel: loaded, factored, stored
-#define V4_PSTAMP(p, ev) do { if (lane == 0) g_v4_pstamps[p][ev] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define V4_STAMP(ev) do { } while (0)
-#define V4_PSTAMP(p, ev) do { } while (0)
-#endif
 // tile row of lower tile t (t = i(i+1)/2 + j)
 __device__ __forceinline__ constexpr int tile_i(int t) {
   return t < 1 ? 0 : t < 3 ? 1 : t < 6 ? 2 : t < 10 ? 3 : t < 15 ? 4 : t < 21 ? 5 : t < 28 ? 6 : 7;
@@ -203,10 +185,8 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
     double* __restrict__ Lout, int64_t ldlo, double* __restrict__ logdiag, int* info, int base,
     int nreal) {
   __shared__ double S[NT * TSZ];
-  __shared__ double M[32];
   __shared__ double DG[128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  V4_STAMP(0);
   // ---- A's lower tiles into LDS (all 18 loads of a thread in flight at once); zeros into
   //      Linv above the tile diagonal
   {
@@ -227,7 +207,6 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
     }
   }
   __syncthreads();
-  V4_STAMP(1);
 
   d4 T[3];                  // the X row in flight: T_k held by the wave that finishes X_{row,k}
   const int uw = wave - 1;  // update-wave index 0..2 in phase A
@@ -244,10 +223,8 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
 #pragma unroll
         for (int c = 0; c < 16; ++c) P[s][c] = R >= t0 ? S[t + c] : 0.0;
       }
-      V4_PSTAMP(p, 0);
-      if (p < 4) factor_panel<0, true>(P, p, lane, M);
-      else factor_panel<1, false>(P, p, lane, M);
-      V4_PSTAMP(p, 1);
+      if (p < 4) factor_panel<0, true>(P, p, lane);
+      else factor_panel<1, false>(P, p, lane);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int R = lane + 64 * s;
@@ -263,7 +240,6 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
             dst[c] = R >= t0 ? (dv2){P[s][2 * c], P[s][2 * c + 1]} : (dv2){0.0, 0.0};
         }
       }
-      V4_PSTAMP(p, 2);
     } else if (p >= 1) {
       const int pp = p - 1;
       // wave 1 + pp % 3 inverts L_{pp,pp} (and takes the logs); the bulk tiles go to the
@@ -287,9 +263,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
         if (k < pp) T[slot] = inv_row_t(S, pp, k, lane);
       }
     }
-    V4_STAMP(2 + 4 * p);
     __syncthreads();
-    V4_STAMP(3 + 4 * p);
     // ================= phase B: all 4 waves — panel p into column p+1 (lookahead) and
     //                   X_{p-1,k} = −X_{p-1,p-1} T_k (by the waves holding T_k); X_77 at p = 7
     if (p < 7) {  // tiles (i, p+1), i = p+1..7: wave w takes i = p+1+w and p+5+w
@@ -317,9 +291,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
         }
       }
     }
-    V4_STAMP(4 + 4 * p);
     __syncthreads();
-    V4_STAMP(5 + 4 * p);
   }
   // ================= tail: X row 7 (T_k on all 4 waves, 7 tile products each), then finish
 #pragma unroll
@@ -327,9 +299,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
     const int k = tail_k(wave, slot);
     if (k >= 0) T[slot] = inv_row_t(S, 7, k, lane);
   }
-  V4_STAMP(37);
   __syncthreads();  // (X row 6 and X_77 were final before; only the reads above precede this)
-  V4_STAMP(38);
   {
     const int td = tix(7, 7);
 #pragma unroll
@@ -345,7 +315,6 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
       }
     }
   }
-  V4_STAMP(39);
   if (tid < 128) {
     // first non-positive pivot (torch.potrf's leading-minor index): a bad pivot makes its
     // L_ii NaN and poisons every later one, so the minimum flagged index is the first
@@ -365,7 +334,6 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
       *reinterpret_cast<dv2*>(Linv + (int64_t)(16 * ui + r) * ldl + 16 * uj + c2) = (dv2){0.0, 0.0};
     }
   }
-  V4_STAMP(36);
 }
 }  // namespace v4
 

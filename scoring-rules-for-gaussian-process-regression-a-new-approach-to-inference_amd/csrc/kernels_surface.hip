@@ -13,6 +13,9 @@
 //                          LOO variance; without the flag c = 1/d, the KF:416-424 form)
 // n ≤ 128: A (n × (n+1) doubles) plus β in dynamic LDS.  A non-PD point (d_k ≤ 0) gives NaN
 // objectives for that point (R's chol would stop the script; the grid keeps going).
+#include <mutex>
+#include <set>
+
 #include "gps_internal.h"
 
 namespace gps {
@@ -118,13 +121,22 @@ hipError_t launch_surface(const SurfaceParams& p, hipStream_t s) {
   if (p.n < 1 || p.n > GPS_SURFACE_MAX_N || p.d < 1 || p.nl < 1 || p.ns < 1)
     return hipErrorInvalidValue;
   const size_t lds = surface_lds_bytes(p.n);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)surface_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)surface_lds_bytes(GPS_SURFACE_MAX_N));
-    if (e != hipSuccess) return e;
-    attr = true;
+  // the dynamic-LDS limit (133 KB at n = 128) is a per-device function attribute: set once per
+  // device under a lock, so contexts on several threads or devices never race on it
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    static std::mutex mu;
+    static std::set<int> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!done.count(dev)) {
+      e = hipFuncSetAttribute((const void*)surface_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)surface_lds_bytes(GPS_SURFACE_MAX_N));
+      if (e != hipSuccess) return e;
+      done.insert(dev);
+    }
   }
   hipLaunchKernelGGL(surface_kernel, dim3((unsigned)(p.nl * p.ns)), dim3(64), lds, s, p);
   return hipGetLastError();

@@ -39,6 +39,7 @@ SIGNATURES = {
     "gps_ctx_stream": (_c_vp, [_c_vp]),
     "gps_ctx_synchronize": (_c_int, [_c_vp]),
     "gps_ctx_set_option": (_c_int, [_c_vp, _c_int, _c_int]),
+    "gps_ctx_stats": (_c_int, [_c_vp, _c_vp]),
     "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
     "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
     "gps_gram": (_c_int, [_c_vp, _c_int, _P, _c_i64, _P, _c_i64, _c_int, _c_dbl, _P, _c_int,
@@ -195,6 +196,14 @@ class Context:
 
     def synchronize(self):
         self.call("gps_ctx_synchronize")
+
+    def stats(self):
+        """{graphs, graph_cap, graph_overflow, device_bytes} (gps_ctx_stats)."""
+        import numpy as np
+        out = np.zeros(4, np.int64)
+        self.call("gps_ctx_stats", out.ctypes.data_as(ctypes.c_void_p))
+        return dict(zip(("graphs", "graph_cap", "graph_overflow", "device_bytes"),
+                        (int(v) for v in out)))
 
     def set_stream(self, stream_handle):
         self.call("gps_ctx_set_stream", _c_vp(stream_handle))

@@ -45,3 +45,35 @@ def nrel(a, b):
 def gpu_ctx():
     import gpscore
     return gpscore.Context(0)
+
+
+# ------------------------------------------------------------------ parity floors record
+# Every measured-floor comparison (the BASELINE configs, the shard splits, the CP.R surfaces)
+# records {test: {output: [gpu-vs-reference error, measured floor, absolute cap]}}; the session
+# writes them to $GPS_PARITY_FLOORS (default gpurun_out/parity_floors.json) so the margins are
+# visible outside pytest's captured output (committed as profiles/r3_parity_floors.json).
+PARITY_FLOORS = {}
+
+
+def record_floors(test, errs, floors, caps):
+    rec = PARITY_FLOORS.setdefault(test, {})
+    for k, e in errs.items():
+        rec[k] = [float(e), float(floors.get(k, float("nan"))), float(caps.get(k, float("nan")))]
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not PARITY_FLOORS:
+        return
+    import json
+    path = os.environ.get("GPS_PARITY_FLOORS", os.path.join(ROOT, "gpurun_out", "parity_floors.json"))
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        old = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                old = json.load(f)
+        old.update(PARITY_FLOORS)
+        with open(path, "w") as f:
+            json.dump(old, f, indent=1, sort_keys=True)
+    except OSError:
+        pass

@@ -9,7 +9,7 @@ the movement a 1e-15 relative perturbation of x causes (measured here on the GPU
 import numpy as np
 import pytest
 
-from conftest import load_golden, nrel
+from conftest import load_golden, nrel, record_floors
 
 pytestmark = pytest.mark.gpu
 
@@ -24,12 +24,19 @@ def test_surface_vs_golden(gpu_ctx, name):
     rng = np.random.default_rng(3)
     xp = g["x"] * (1 + 1e-15 * rng.standard_normal(g["x"].shape))
     pert = gpscore.surface(xp, g["y"], g["ell"], g["sd"], ctx=gpu_ctx)
+    errs, floors = {}, {}
     for k, nm in enumerate(NAMES):
-        err = nrel(got[nm], g["surf"][k])
-        floor = nrel(pert[nm], got[nm])
-        print(f"{name} {nm:14s} gpu-vs-golden {err:.2e}  floor {floor:.2e}")
+        errs[nm] = nrel(got[nm], g["surf"][k])
+        floors[nm] = nrel(pert[nm], got[nm])
+    # absolute ceiling: n ≤ 100 points with σ ≥ the grid's smallest s, cond(A) ≤ n·sf²/s²_min
+    cap = 50.0 * len(g["x"]) / float(np.min(g["sd"])) ** 2 * np.finfo(np.float64).eps + 1e-12
+    record_floors(name, errs, floors, {nm: cap for nm in NAMES})
+    for nm in NAMES:
+        err, floor = errs[nm], floors[nm]
+        print(f"{name} {nm:14s} gpu-vs-golden {err:.2e}  floor {floor:.2e}  cap {cap:.2e}")
         assert np.all(np.isfinite(got[nm]))
         assert err <= 30 * floor + 1e-12, (nm, err, floor)
+        assert max(err, floor) <= cap, (nm, err, floor, cap)
 
 
 def test_surface_matches_single_point_fits(gpu_ctx):
@@ -69,3 +76,31 @@ def test_surface_edge_cases(gpu_ctx):
     assert np.all(np.isnan(s["nlml"][0])) and np.all(np.isfinite(s["nlml"][1]))
     with pytest.raises(gpscore.GpsError):
         gpscore.surface(np.zeros((129, 1)), np.zeros(129), [1.0], [0.1], ctx=gpu_ctx)
+
+
+def test_surface_concurrent_contexts():
+    """Two host threads, each with its own context, call gps_full_surface at n = 128 (the
+    133 KB dynamic-LDS configuration) at the same time: the per-device launch attribute is set
+    once under a lock, so both grids match the single-threaded result bitwise."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import gpscore
+    rng = np.random.default_rng(21)
+    x = rng.uniform(-3, 3, (128, 2))
+    y = np.sin(x.sum(1))
+    ell, sd = np.linspace(0.5, 2.0, 7), np.linspace(0.05, 0.5, 5)
+
+    def job(_):
+        ctx = gpscore.Context(0)
+        try:
+            return [gpscore.surface(x, y, ell, sd, ctx=ctx) for _ in range(3)]
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        runs = [r for rs in ex.map(job, range(2)) for r in rs]
+    ref = job(0)[0]
+    for r in runs:
+        for nm in NAMES:
+            assert np.array_equal(r[nm], ref[nm]), nm
+            assert np.all(np.isfinite(r[nm]))

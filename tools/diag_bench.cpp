@@ -105,31 +105,9 @@ static int run(const char* name, LeafFn launch_potrf_diag) {
   return ok ? 0 : 1;
 }
 
-static void print_stamps() {
-#ifdef GPS_V4_STAMPS
-  long long st[4][40];
-  hipMemcpyFromSymbol(st, HIP_SYMBOL(v4::g_v4_stamps), sizeof(st));
-  const long long t0 = st[0][0];
-  printf("v4 stamps (cycles from start): load done w0 %lld w1 %lld\n", st[0][1] - t0, st[1][1] - t0);
-  for (int p = 0; p < 8; ++p)
-    printf("  p=%d  A-end w0 %6lld w1 %6lld w2 %6lld w3 %6lld | B-start %6lld | B-end w1 %6lld w2 %6lld w3 %6lld | next %6lld\n", p,
-           st[0][2 + 4 * p] - t0, st[1][2 + 4 * p] - t0, st[2][2 + 4 * p] - t0, st[3][2 + 4 * p] - t0,
-           st[0][3 + 4 * p] - t0, st[1][4 + 4 * p] - t0, st[2][4 + 4 * p] - t0, st[3][4 + 4 * p] - t0,
-           st[0][5 + 4 * p] - t0);
-  long long ps[8][3];
-  hipMemcpyFromSymbol(ps, HIP_SYMBOL(v4::g_v4_pstamps), sizeof(ps));
-  for (int p = 0; p < 8; ++p)
-    printf("  pivot p=%d: load %lld, factor %lld, store %lld cycles\n", p,
-           ps[p][0] - (p ? st[0][5 + 4 * (p - 1)] : st[0][1]), ps[p][1] - ps[p][0], ps[p][2] - ps[p][1]);
-  for (int w = 0; w < 4; ++w)
-    printf("  tail w%d: T done %lld, barrier %lld, finish %lld, end %lld\n", w, st[w][37] - t0,
-           st[w][38] - t0, st[w][39] - t0, st[w][36] - t0);
-#endif
-}
-
 int main(int argc, char** argv) {
   int rc = run("library leaf v4 (MFMA, kernels_potrf.hip)", launch_potrf_leaf);
-  print_stamps();
+  
   rc |= run("round-1 leaf v3 (register-blocked, tools/leaf_v3.hip)", leafv3::launch_potrf_leaf_v3);
   if (argc < 2 || strcmp(argv[1], "lib") != 0) rc |= run("MFMA-tiled leaf (tools/leaf_mfma.hip)", launch_potrf_leaf_mfma);
   return rc;

@@ -5,8 +5,4 @@ set -e
 C=scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd/csrc
 F="-O3 --offload-arch=gfx950 -std=c++17 -Iinclude -mllvm -amdgpu-mfma-vgpr-form=1 -Wno-unused-value"
 hipcc $F -I$C -Itools tools/diag_bench.cpp -o /tmp/db
-hipcc $F -DGPS_V4_STAMPS -I$C -Itools tools/diag_bench.cpp -o /tmp/db_st
-timeout -k 5 60 /tmp/db_st lib | grep -A22 "v4 stamps"
-hipcc $F -DGPS_V4_PIVOT_LDS -I$C -Itools tools/diag_bench.cpp -o /tmp/db_rl
-echo "== pivot multipliers by LDS broadcast"; timeout -k 5 60 /tmp/db_rl lib | head -8
 for rep in 1 2; do timeout -k 5 60 /tmp/db "$@"; done
