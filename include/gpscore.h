@@ -86,6 +86,13 @@ enum {
                             q_i = ‖Lm⁻¹k_i‖² that need only the top-level Lm11⁻¹ (a quarter of
                             the pass) on a second stream while the rest of Lm's factorisation
                             runs; 0: the whole pass after it.  Same tiles, same results. */
+  GPS_OPT_DAG = 12,      /* 1 (default): diagonal blocks of at most GPS_OPT_DAG_TILES 128-tiles
+                            at the bottom of the recursive factorisation are factored and
+                            inverted by ONE persistent launch (a device task queue of tile
+                            products, per-tile arrival counters); 0: the recursion down to
+                            the 128-block leaf.  Same algorithm, other summation order. */
+  GPS_OPT_DAG_TILES = 13, /* largest block (in 128-tiles, 2..64, default 20) the persistent
+                            factorisation takes */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
@@ -98,6 +105,12 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 enum { GPS_STAT_GRAPHS = 0, GPS_STAT_GRAPH_CAP = 1, GPS_STAT_GRAPH_OVERFLOW = 2,
        GPS_STAT_DEVICE_BYTES = 3, GPS_N_STATS = 4 };
 int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
+
+/* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one
+ * word per strip task (type | part << 3 | i << 8 | j << 16 | k << 24; types 0 LEAF, 1 TRSM,
+ * 2 UPD, 3 UPDX, 4 FIN — kernels_potrf.hip).  Returns the queue length (writes at most cap
+ * words); needs no device. */
+int gps_dag_task_list(int T, uint32_t* out, int cap);
 
 /* on: 0 off, 1 per-kernel-class tags, 2 GEMM tags also carry layout/shape/tri/split-K/lda */
 int gps_prof_enable(gps_ctx* ctx, int on);

@@ -97,6 +97,11 @@ struct gps_ctx {
   size_t sync_used = 0;
   bool graphs = true;                  // GPS_OPT_GRAPH: replay the factorisation from a hipGraph
   bool pred_pre = true;                // GPS_OPT_PRED_PRE
+  bool dag = true;                     // GPS_OPT_DAG: persistent factorisation of the bottom blocks
+  int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
+  std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
+  DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
+  int64_t dag_cnt_used = 0;
   struct PrePass {                     // work potrf_inv launches on aux[0] once the top-level
     int kind = 0;                      // L11⁻¹ is final: PRE_FITC_Q (the q column tiles [0, n1))
     int64_t n1 = 0;
@@ -374,6 +379,22 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
   return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
 
+// a block of nb 128-tiles goes to the persistent factorisation (GPS_OPT_DAG)
+bool dag_block(const gps_ctx* ctx, int64_t nb) { return ctx->dag && nb >= 2 && nb <= ctx->dag_tiles; }
+
+// the block sizes the recursion of an nb-tile factorisation hands to the persistent kernel, and
+// how many counter ints all of them need together
+void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t& cnt) {
+  if (nb <= 1) return;
+  if (dag_block(ctx, nb)) {
+    sizes.push_back((int)nb);
+    cnt += dag_cnt_ints((int)nb);
+    return;
+  }
+  dag_blocks(ctx, nb / 2, sizes, cnt);
+  dag_blocks(ctx, nb - nb / 2, sizes, cnt);
+}
+
 // recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
 // W is this level's workspace (n1·n2 doubles); deeper levels on the A22 side get
 // the region after it, so a concurrent GEMM that still reads this level's W never
@@ -391,6 +412,23 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   if (nb == 1) {
     Prof pr(ctx, "potrf_diag128", 2.0 * 128 * 128 * 128 / 3.0, 0);
     HIPCHK(launch_potrf_leaf(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, s));
+    return 0;
+  }
+  if (dag_block(ctx, nb)) {  // the whole block in one persistent launch (kernels_potrf.hip)
+    auto it = ctx->dag_lists.find(nb);
+    const int64_t need = dag_cnt_ints(nb);
+    if (it == ctx->dag_lists.end() || ctx->dag_cnt_used + need > (int64_t)(ctx->dag_cnt.cap / 4))
+      return fail(ctx, -2, "persistent factorisation: task list / counters not prepared");
+    DagParams d;
+    d.A = A; d.lda = lda; d.Linv = Linv; d.ldl = ldl; d.Lout = Lout; d.ldlo = ldlo;
+    d.logdiag = logdiag; d.info = info; d.base = base; d.nreal = nreal; d.T = nb;
+    d.tasks = static_cast<const uint32_t*>(it->second.first.p); d.ntasks = it->second.second;
+    d.cnt = static_cast<int*>(ctx->dag_cnt.p) + ctx->dag_cnt_used;
+    d.spin_ticks = 200000000ull;  // 2 s at the 100 MHz real-time clock
+    ctx->dag_cnt_used += need;
+    const double nn = 128.0 * nb;
+    Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
+    HIPCHK(launch_potrf_dag(d, std::min(ctx->ncu, std::max(4, 2 * nb * nb)), s));
     return 0;
   }
   const int n1b = nb / 2, n2b = nb - n1b;
@@ -478,8 +516,8 @@ size_t potrf_ws_doubles(int64_t n_pad) {
 
 // factor the padded SPD matrix in A (destroyed) into Linv (must be zero in strict-upper
 // tiles), logdiag (n_pad).  Returns 0 or the LAPACK-style info (> 0).
-int reset_info(gps_ctx* ctx) {
-  HIPCHK(hipMemsetAsync(ctx->info.p, 0x7f, sizeof(int), ctx->stream));
+int reset_info(gps_ctx* ctx) {  // [first non-PD minor, persistent-kernel error]
+  HIPCHK(hipMemsetAsync(ctx->info.p, 0x7f, 2 * sizeof(int), ctx->stream));
   return 0;
 }
 
@@ -492,9 +530,28 @@ constexpr size_t kMaxGraphs = 256;
 
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
+  // persistent blocks: task lists per size (uploaded once, before any capture) and one zeroed
+  // counter region per launch of this call (a memset node ahead of the sequence)
+  std::vector<int> dsizes;
+  int64_t dcnt = 0;
+  dag_blocks(ctx, n_pad / GPS_TILE, dsizes, dcnt);
+  for (int T : dsizes) {
+    if (ctx->dag_lists.count(T)) continue;
+    const std::vector<uint32_t> tl = dag_task_list(T);
+    auto& e = ctx->dag_lists[T];
+    HIPCHK(ensure(e.first, tl.size() * 4));
+    HIPCHK(hipMemcpy(e.first.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice));
+    e.second = (int)tl.size();
+  }
+  if (dcnt) HIPCHK(ensure(ctx->dag_cnt, (size_t)dcnt * 4));
   auto eager = [&]() {
     ctx->sync_used = 0;
     ctx->pre.join = nullptr;
+    ctx->dag_cnt_used = 0;
+    if (dcnt) {
+      hipError_t e = hipMemsetAsync(ctx->dag_cnt.p, 0, (size_t)dcnt * 4, ctx->stream);
+      if (e != hipSuccess) return fail(ctx, -2, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+    }
     return potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
                          static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad, true);
   };
@@ -509,7 +566,8 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       // the pre-pass's operands (only when it is part of the sequence)
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
-      pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0};
+      pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
+      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_cnt.p};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
@@ -555,8 +613,10 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
 }
 
 int check_info(gps_ctx* ctx) {
-  HIPCHK(hipMemcpyAsync(ctx->hinfo, ctx->info.p, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->hinfo, ctx->info.p, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->hinfo[1] != 0x7f7f7f7f)
+    return fail(ctx, -4, "persistent factorisation: a task's dependency wait timed out (internal error)");
   const int info = *ctx->hinfo;
   if (info != 0x7f7f7f7f) {
     char buf[160];
@@ -1048,7 +1108,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
                  &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW};
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->dag_cnt};
 }
 
 extern "C" {
@@ -1091,6 +1151,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   leave_local_group(ctx);
   for (DBuf* b : ctx_buffers(ctx)) release(*b);
+  for (auto& kv : ctx->dag_lists) release(kv.second.first);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join})
@@ -1132,6 +1193,11 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
     case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;
+    case GPS_OPT_DAG: ctx->dag = value != 0; return 0;
+    case GPS_OPT_DAG_TILES:
+      ARGCHK(value >= 2 && value <= 64, "GPS_OPT_DAG_TILES must be in 2..64");
+      ctx->dag_tiles = value;
+      return 0;
     default: return fail(ctx, -1, "unknown option");
   }
 }
@@ -1154,6 +1220,13 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
   out[GPS_STAT_GRAPH_OVERFLOW] = ctx->graph_overflow;
   out[GPS_STAT_DEVICE_BYTES] = (int64_t)bytes;
   return 0;
+}
+
+int gps_dag_task_list(int T, uint32_t* out, int cap) {
+  if (T < 2 || T > 64 || cap < 0 || (cap > 0 && !out)) return fail(nullptr, -1, "bad arguments");
+  const std::vector<uint32_t> tl = dag_task_list(T);
+  for (int i = 0; i < cap && i < (int)tl.size(); ++i) out[i] = tl[i];
+  return (int)tl.size();
 }
 
 int gps_prof_enable(gps_ctx* ctx, int on) {
@@ -1770,7 +1843,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
                  ctx->Knm.d(), mp, (int)np, (int)mp)))
     return rc;
-  const bool preq = ctx->pred_pre && mp > GPS_TILE;
+  // (a persistent top level has no recursion step to overlap the pre-pass with)
+  const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
   const int64_t qn1 = preq ? (mp / GPS_TILE / 2) * GPS_TILE : 0;
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;

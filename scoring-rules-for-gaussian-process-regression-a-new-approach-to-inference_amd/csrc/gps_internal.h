@@ -176,6 +176,24 @@ hipError_t launch_potrf_leaf(const double* A, int64_t lda, double* Linv, int64_t
                              double* Lout, int64_t ldlo, double* logdiag, int* info,
                              int base, int n_real_in_block, hipStream_t s);
 
+// persistent tiled factorisation of a diagonal block of T tiles (kernels_potrf.hip): L⁻¹ into
+// Linv, L into A's strictly-lower tiles (and Lout if given), logdiag, info[0] as the leaf;
+// info[1] != 0x7f7f7f7f on a lost dependency (bounded spin).  cnt: 16 + 2·T² ints, zeroed
+// before the launch; tasks: dag_task_list(T) on the device.
+struct DagParams {
+  double* A; int64_t lda;
+  double* Linv; int64_t ldl;
+  double* Lout; int64_t ldlo;
+  double* logdiag; int* info; int base; int nreal;
+  int T;
+  const uint32_t* tasks; int ntasks;
+  int* cnt;
+  unsigned long long spin_ticks;   // 100 MHz s_memrealtime ticks a dependency wait may take
+};
+hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
+std::vector<uint32_t> dag_task_list(int T);
+inline int64_t dag_cnt_ints(int T) { return (16 + 2 * (int64_t)T * T + 63) / 64 * 64; }
+
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)
 hipError_t launch_gemv_lower(const double* L, int64_t ldl, const double* x, double* y,
                              int n_pad, hipStream_t s);

@@ -3,6 +3,10 @@
 // recursive factorisation (csrc/api.hip potrf_inv_rec), one 128×128 block per launch.
 // (The round-1 register-blocked VALU kernel, 51 µs, is kept outside the library as the A/B
 // baseline: tools/leaf_v3.hip, tools/diag_bench.cpp.)
+#include <algorithm>
+#include <queue>
+#include <vector>
+
 #include "gps_internal.h"
 
 namespace gps {
@@ -36,6 +40,37 @@ __device__ __forceinline__ double rl(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
   return __hiloint2double(hi, lo);
+}
+// Coherent (write-through, L1-bypassing: `sc1`) element access for data handed between the
+// workgroups of one launch (the persistent factorisation below); plain access otherwise.
+template <bool COH>
+__device__ __forceinline__ void st_d(double* p, double v) {
+  if constexpr (COH)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                       (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+template <bool COH>
+__device__ __forceinline__ void st_d2(double* p, dv2 v) {
+  if constexpr (COH) {
+    st_d<true>(p, v.x);
+    st_d<true>(p + 1, v.y);
+  } else {
+    *reinterpret_cast<dv2*>(p) = v;
+  }
+}
+template <bool COH>
+__device__ __forceinline__ dv2 ld_d2(const double* p) {
+  if constexpr (COH) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (dv2){__longlong_as_double((long long)a), __longlong_as_double((long long)b)};
+  } else {
+    return *reinterpret_cast<const dv2*>(p);
+  }
 }
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -118,6 +153,7 @@ __device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane
 
 // X_pp = L_pp⁻¹ (16×16 lower; lane c < 16 forms column c by right-looking substitution, so the
 // dependent chain is one FMA + one multiply per row) into slot (p,p) and Linv
+template <bool COH>
 __device__ __forceinline__ void invert_diag(double* S, double* DG, int p, int lane,
                                             double* Linv, int64_t ldl) {
   const int t = tix(p, p);
@@ -141,7 +177,7 @@ __device__ __forceinline__ void invert_diag(double* S, double* DG, int p, int la
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       S[t * TSZ + i * TS + lane] = x[i];
-      Linv[(int64_t)(16 * p + i) * ldl + 16 * p + lane] = x[i];
+      st_d<COH>(Linv + (int64_t)(16 * p + i) * ldl + 16 * p + lane, x[i]);
     }
   }
 }
@@ -180,12 +216,15 @@ __device__ __forceinline__ int tail_k(int wave, int slot) {
   return slot == 0 ? wave : (wave == 0 ? -1 : 7 - wave);
 }
 
-__global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
-    const double* __restrict__ A, int64_t lda, double* __restrict__ Linv, int64_t ldl,
-    double* __restrict__ Lout, int64_t ldlo, double* __restrict__ logdiag, int* info, int base,
-    int nreal) {
-  __shared__ double S[NT * TSZ];
-  __shared__ double DG[128];
+// The leaf as a device function of one 256-thread workgroup: the stand-alone kernel below
+// (COH = false) and the persistent factorisation's LEAF task (COH = true: A read and L⁻¹ written
+// coherently, since other workgroups of the same launch produce / consume them).  S, DG: LDS.
+template <bool COH>
+__device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t lda,
+                                          double* __restrict__ Linv, int64_t ldl,
+                                          double* __restrict__ Lout, int64_t ldlo,
+                                          double* __restrict__ logdiag, int* info, int base,
+                                          int nreal, double* S, double* DG) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // ---- A's lower tiles into LDS (all 18 loads of a thread in flight at once); zeros into
   //      Linv above the tile diagonal
@@ -197,7 +236,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
     for (int m = 0; m < 18; ++m) {
       const int ti = hb ? tile_i(2 * m + 1) : tile_i(2 * m);
       const int tj = hb ? 2 * m + 1 - tix(tile_i(2 * m + 1), 0) : 2 * m - tix(tile_i(2 * m), 0);
-      v[m] = *reinterpret_cast<const dv2*>(A + (int64_t)(16 * ti + r) * lda + 16 * tj + c2);
+      v[m] = ld_d2<COH>(A + (int64_t)(16 * ti + r) * lda + 16 * tj + c2);
     }
 #pragma unroll
     for (int m = 0; m < 18; ++m) {
@@ -254,7 +293,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
           if (who == rank) tile_update(S, tix(i, j), tix(i, pp), tix(j, pp), lane);
         }
       if (rank == 0) {
-        invert_diag(S, DG, pp, lane, Linv, ldl);
+        invert_diag<COH>(S, DG, pp, lane, Linv, ldl);
         if (lane < 16) logdiag[16 * pp + lane] = log(DG[16 * pp + lane]);
       }
 #pragma unroll
@@ -271,7 +310,7 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
       if (i1 < 8) tile_update2(S, tix(i0, p + 1), tix(i0, p), tix(i1, p + 1), tix(i1, p), tb, lane);
       else if (i0 < 8) tile_update(S, tix(i0, p + 1), tix(i0, p), tb, lane);
     } else if (wave == 0) {
-      invert_diag(S, DG, 7, lane, Linv, ldl);
+      invert_diag<COH>(S, DG, 7, lane, Linv, ldl);
     }
     if (p >= 1 && wave != 0) {
       const int pp = p - 1, td = tix(pp, pp);
@@ -286,7 +325,8 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             S[acc_off(tdst, lane, q)] = acc[q];
-            Linv[(int64_t)(16 * pp + 4 * q + (lane >> 4)) * ldl + 16 * k + (lane & 15)] = acc[q];
+            st_d<COH>(Linv + (int64_t)(16 * pp + 4 * q + (lane >> 4)) * ldl + 16 * k + (lane & 15),
+                      acc[q]);
           }
         }
       }
@@ -311,7 +351,8 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
         for (int kk = 0; kk < 4; ++kk) acc = mfma(-opnd(S, td, lane, kk), T[slot][kk], acc);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          Linv[(int64_t)(16 * 7 + 4 * q + (lane >> 4)) * ldl + 16 * k + (lane & 15)] = acc[q];
+          st_d<COH>(Linv + (int64_t)(16 * 7 + 4 * q + (lane >> 4)) * ldl + 16 * k + (lane & 15),
+                    acc[q]);
       }
     }
   }
@@ -331,11 +372,384 @@ __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
       const int ui = u < 7 ? 0 : u < 13 ? 1 : u < 18 ? 2 : u < 22 ? 3 : u < 25 ? 4 : u < 27 ? 5 : 6;
       const int ustart = ui * 7 - ui * (ui - 1) / 2;  // first upper tile of row ui
       const int uj = ui + 1 + (u - ustart);
-      *reinterpret_cast<dv2*>(Linv + (int64_t)(16 * ui + r) * ldl + 16 * uj + c2) = (dv2){0.0, 0.0};
+      st_d2<COH>(Linv + (int64_t)(16 * ui + r) * ldl + 16 * uj + c2, (dv2){0.0, 0.0});
     }
   }
 }
+
+__global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
+    const double* __restrict__ A, int64_t lda, double* __restrict__ Linv, int64_t ldl,
+    double* __restrict__ Lout, int64_t ldlo, double* __restrict__ logdiag, int* info, int base,
+    int nreal) {
+  __shared__ double S[NT * TSZ];
+  __shared__ double DG[128];
+  leaf_body<false>(A, lda, Linv, ldl, Lout, ldlo, logdiag, info, base, nreal, S, DG);
+}
 }  // namespace v4
+
+// ---------------------------------------------------------------------------
+// Persistent tiled factorisation of a diagonal block of T ≤ 64 tiles (128 columns each): L and
+// L⁻¹ in ONE launch.  The bottom of the recursion (potrf_inv_rec in api.hip) used to be a chain
+// of ~7 dependent launches per 128 columns (leaf, the TRSM / SYRK / T / TRMM products of every
+// recursion level), each a few µs of work behind a ~5 µs launch boundary with most of the chip
+// idle; here one workgroup per CU pulls tasks from a device queue, waits for their inputs through
+// per-tile arrival counters and publishes its outputs write-through, so the chain costs the
+// leaves plus a cross-workgroup hand-off (~µs) per dependent product.
+//
+// Tasks (tile indices in the block; L_ik lands in A_ik, X = L⁻¹ in Linv):
+//   LEAF(k)        [L_kk, X_kk] = leaf(A_kk)                                  (one workgroup)
+//   TRSM(i,k)      L_ik  = A_ik · X_kkᵀ                        i > k          (4 row strips)
+//   UPD(i,j,k)     A_ij −= L_ik · L_jkᵀ                        i ≥ j > k      (4 row strips)
+//   UPDX(i,k,j)    S_ik (+)= L_ij · X_jk  (first term: =)      i > j ≥ k      (4 row strips)
+//   FIN(i,k)       X_ik  = −X_ii · S_ik   (in place)           i > k          (4 column strips)
+// (right-looking Cholesky; the inverse right-looking too: X_ik = −X_ii Σ_{j=k}^{i−1} L_ij X_jk,
+// S_ik accumulated in X's own tile).  Each strip task runs on 4 waves, each a 32×32 block of
+// v_mfma_f64_16x16x4 with its operands streamed from L2 (no LDS), the K range clipped to the
+// triangular operand's nonzeros.  Arrival counters per tile: A-side acnt[i][j] (+4 per UPD, +4
+// per TRSM, +1 per LEAF) and X-side xcnt[i][k] (+4 per UPDX / FIN, +1 per LEAF); a task polls
+// the counts it needs (one lane, relaxed agent-scope loads, bounded) — every input of a task
+// was written by tasks earlier in the queue, so the queue order (a topological order, host
+// side: dag_task_list) guarantees progress for any residency.  Hand-offs follow the
+// write-through form of cdna_hip_programming.md §6 Guideline 16: payload stores `sc1`, every
+// wave drains (vmcnt 0), barrier, one relaxed agent atomic add; consumers load `sc1`.
+namespace dag {
+using v4::d4;
+using v4::dv2;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+constexpr int NP = 4;        // strips per tile task
+constexpr int AUX_SC1 = 16;  // cache-policy bits of the buffer intrinsics: sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ dv2 ld128(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX_SC1));
+}
+__device__ __forceinline__ double ld64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX_SC1));
+}
+__device__ __forceinline__ void st64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, off, 0, AUX_SC1);
+}
+__device__ __forceinline__ int ld_cnt(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave: acc = A (32 rows, k in [kb, ke), lda) · B, B stored [k][j] (BT = false, 32 columns)
+// or [j][k] (BT = true, 32 rows); operand fragments straight from L2 (sc1) in groups of two
+// 16-deep chunks, one group ahead of the MFMAs (the layout of gemm_f64_small_kernel)
+template <bool BT>
+__device__ __forceinline__ void wave_gemm32(const double* Ap, int64_t lda, const double* Bp,
+                                            int64_t ldb, int kb, int ke, d4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(Ap, (uint32_t)(32 * lda * 8));
+  const __amdgpu_buffer_rsrc_t rb = rsrc(Bp, (uint32_t)((BT ? 32 : 128) * ldb * 8));
+  typedef double Frag[2][2][4];  // [chunk in group][16-block][k step]
+  auto load_group = [&](int c, Frag& a, Frag& b) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = kb + 16 * (c + u) + 4 * g;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t oa = (uint32_t)(((int64_t)(16 * i + r) * lda + k) * 8);
+        const dv2 a0 = ld128(ra, oa), a1 = ld128(ra, oa + 16);
+        a[u][i][0] = a0.x; a[u][i][1] = a0.y; a[u][i][2] = a1.x; a[u][i][3] = a1.y;
+        if constexpr (BT) {
+          const uint32_t ob = (uint32_t)(((int64_t)(16 * i + r) * ldb + k) * 8);
+          const dv2 b0 = ld128(rb, ob), b1 = ld128(rb, ob + 16);
+          b[u][i][0] = b0.x; b[u][i][1] = b0.y; b[u][i][2] = b1.x; b[u][i][3] = b1.y;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            b[u][i][e] = ld64(rb, (uint32_t)(((int64_t)(k + e) * ldb + 16 * i + r) * 8));
+        }
+      }
+    }
+  };
+  auto mma_group = [&](const Frag& a, const Frag& b) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][i][kk], b[u][j][kk], acc[i][j], 0, 0, 0);
+  };
+  const int nc = (ke - kb) / 16;  // even: kb, ke are multiples of 32
+  Frag fa0, fb0, fa1, fb1;
+  int c = 0;
+  if (c < nc) load_group(c, fa0, fb0);
+  while (c < nc) {
+    if (c + 2 < nc) load_group(c + 2, fa1, fb1);
+    mma_group(fa0, fb0);
+    c += 2;
+    if (c >= nc) break;
+    if (c + 2 < nc) load_group(c + 2, fa0, fb0);
+    mma_group(fa1, fb1);
+    c += 2;
+  }
+}
+
+struct Strip {          // one wave's 32×32 block of a strip task
+  const double* A; int64_t lda;
+  const double* B; int64_t ldb; int bt;
+  double* C; int64_t ldc;
+  double* C2; int64_t ldc2;   // optional plain copy of the result (L into Lout)
+  double alpha, beta;
+  int kb, ke, active;
+};
+
+// all four waves: compute, barrier (in-place tasks: every read of the strip precedes every
+// write), then write-through stores
+__device__ __forceinline__ void run_strip(const Strip& s) {
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rc = rsrc(s.C, (uint32_t)(32 * s.ldc * 8));
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  double cold[2][2][4];
+  if (s.active) {
+    if (s.beta != 0.0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            cold[i][j][e] = ld64(rc, (uint32_t)(((int64_t)(16 * i + g + 4 * e) * s.ldc + 16 * j + r) * 8));
+    }
+    if (s.bt) wave_gemm32<true>(s.A, s.lda, s.B, s.ldb, s.kb, s.ke, acc);
+    else wave_gemm32<false>(s.A, s.lda, s.B, s.ldb, s.kb, s.ke, acc);
+  }
+  __syncthreads();
+  if (!s.active) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        double v = s.alpha * acc[i][j][e];
+        if (s.beta != 0.0) v = fma(s.beta, cold[i][j][e], v);
+        const int64_t row = 16 * i + g + 4 * e, col = 16 * j + r;
+        st64(rc, (uint32_t)((row * s.ldc + col) * 8), v);
+        if (s.C2) s.C2[row * s.ldc2 + col] = v;
+      }
+}
+
+__global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
+  __shared__ double S[v4::NT * v4::TSZ];
+  __shared__ double DG[128];
+  __shared__ unsigned int sh[2];  // [task word, abort]
+  const int tid = threadIdx.x;
+  const int T = p.T;
+  int* head = p.cnt;
+  int* acnt = p.cnt + 16;
+  int* xcnt = acnt + T * T;
+  int* err = p.info + 1;
+  for (;;) {
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sh[0] = t < p.ntasks ? p.tasks[t] : 0xffffffffu;
+      sh[1] = 0;
+    }
+    __syncthreads();
+    const unsigned int w = __builtin_amdgcn_readfirstlane(sh[0]);
+    if (w == 0xffffffffu) break;
+    const int type = w & 7, part = (w >> 3) & 3, ti = (w >> 8) & 255, tj = (w >> 16) & 255,
+              tk = (w >> 24) & 255;
+    // ---- the counts this task needs (see the header); up to three
+    if (tid == 0) {
+      const int* c0 = nullptr; const int* c1 = nullptr; const int* c2 = nullptr;
+      int v0 = 0, v1 = 0, v2 = 0;
+      switch (type) {
+        case 0:  // LEAF(k = ti)
+          c0 = acnt + ti * T + ti; v0 = NP * ti;
+          break;
+        case 1:  // TRSM(i, k)
+          c0 = acnt + ti * T + tk; v0 = NP * tk;
+          c1 = acnt + tk * T + tk; v1 = NP * tk + 1;
+          break;
+        case 2:  // UPD(i, j, k)
+          c0 = acnt + ti * T + tk; v0 = NP * (tk + 1);
+          c1 = acnt + tj * T + tk; v1 = NP * (tk + 1);
+          c2 = acnt + ti * T + tj; v2 = NP * tk;
+          break;
+        case 3:  // UPDX(i, k, j): L_ij final, X_jk final, S_ik's earlier terms
+          c0 = acnt + ti * T + tj; v0 = NP * (tj + 1);
+          c1 = xcnt + tj * T + tk; v1 = tj == tk ? 1 : NP * (tj - tk + 1);
+          c2 = xcnt + ti * T + tk; v2 = NP * (tj - tk);
+          break;
+        default:  // FIN(i, k)
+          c0 = xcnt + ti * T + tk; v0 = NP * (ti - tk);
+          c1 = xcnt + ti * T + ti; v1 = 1;
+          break;
+      }
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ok = ld_cnt(c0) >= v0;
+        if (ok && c1) ok = ld_cnt(c1) >= v1;
+        if (ok && c2) ok = ld_cnt(c2) >= v2;
+        if (ok) break;
+        if (ld_cnt(err) != 0x7f7f7f7f) { sh[1] = 1; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {  // a lost dependency
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sh[1] = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no loads above the poll
+    }
+    __syncthreads();
+    if (sh[1]) break;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t lda = p.lda, ldl = p.ldl;
+    int* out = nullptr;
+    if (type == 0) {
+      const int64_t o = (int64_t)128 * ti;
+      v4::leaf_body<true>(p.A + o * lda + o, lda, p.Linv + o * ldl + o, ldl,
+                          p.Lout ? p.Lout + o * p.ldlo + o : nullptr, p.ldlo, p.logdiag + o,
+                          p.info, p.base + (int)o, p.nreal - (int)o, S, DG);
+      out = acnt + ti * T + ti;
+    } else {
+      Strip st;
+      st.C2 = nullptr;
+      st.ldc2 = 0;
+      st.active = 1;
+      const int64_t R = 128 * (int64_t)ti, q = 32 * part, wv = 32 * wave;
+      switch (type) {
+        case 1: {  // TRSM(i, k): row strip q of L_ik = A_ik · X_kkᵀ, columns wv..
+          const int64_t K = 128 * (int64_t)tk;
+          st.A = p.A + (R + q) * lda + K; st.lda = lda;
+          st.B = p.Linv + (K + wv) * ldl + K; st.ldb = ldl; st.bt = 1;
+          st.C = p.A + (R + q) * lda + K + wv; st.ldc = lda;
+          if (p.Lout) { st.C2 = p.Lout + (R + q) * p.ldlo + K + wv; st.ldc2 = p.ldlo; }
+          st.alpha = 1.0; st.beta = 0.0; st.kb = 0; st.ke = (int)wv + 32;
+          out = acnt + ti * T + tk;
+          break;
+        }
+        case 2: {  // UPD(i, j, k): row strip q of A_ij −= L_ik L_jkᵀ (diagonal: lower blocks)
+          const int64_t J = 128 * (int64_t)tj, K = 128 * (int64_t)tk;
+          st.A = p.A + (R + q) * lda + K; st.lda = lda;
+          st.B = p.A + (J + wv) * lda + K; st.ldb = lda; st.bt = 1;
+          st.C = p.A + (R + q) * lda + J + wv; st.ldc = lda;
+          st.alpha = -1.0; st.beta = 1.0; st.kb = 0; st.ke = 128;
+          st.active = !(ti == tj && wave > part);
+          out = acnt + ti * T + tj;
+          break;
+        }
+        case 3: {  // UPDX(i, k, j): row strip q of S_ik (+)= L_ij X_jk (X_kk lower: k' >= col)
+          const int64_t J = 128 * (int64_t)tj, K = 128 * (int64_t)tk;
+          st.A = p.A + (R + q) * lda + J; st.lda = lda;
+          st.B = p.Linv + J * ldl + K + wv; st.ldb = ldl; st.bt = 0;
+          st.C = p.Linv + (R + q) * ldl + K + wv; st.ldc = ldl;
+          st.alpha = 1.0; st.beta = tj == tk ? 0.0 : 1.0;
+          st.kb = tj == tk ? (int)wv : 0; st.ke = 128;
+          out = xcnt + ti * T + tk;
+          break;
+        }
+        default: {  // FIN(i, k): column strip q of X_ik = −X_ii S_ik, rows wv.. (X_ii lower)
+          const int64_t K = 128 * (int64_t)tk;
+          st.A = p.Linv + (R + wv) * ldl + R; st.lda = ldl;
+          st.B = p.Linv + R * ldl + K + q; st.ldb = ldl; st.bt = 0;
+          st.C = p.Linv + (R + wv) * ldl + K + q; st.ldc = ldl;
+          st.alpha = -1.0; st.beta = 0.0; st.kb = 0; st.ke = (int)wv + 32;
+          out = xcnt + ti * T + tk;
+          break;
+        }
+      }
+      run_strip(st);
+    }
+    // ---- publish: every wave's write-through stores drained, then one arrival
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (type == 0)
+        __hip_atomic_fetch_add(xcnt + ti * T + ti, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+}  // namespace dag
+
+hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
+  if ((p.lda & 1) || (p.ldl & 1) || (p.Lout && (p.ldlo & 1)) || p.T < 1 || p.T > 64 || nwg < 1 ||
+      !p.tasks || !p.cnt || p.ntasks < 1)
+    return hipErrorInvalidValue;
+  // every strip's buffer descriptor spans at most 128 rows of its matrix (32-bit offsets)
+  if ((int64_t)128 * std::max(p.lda, p.ldl) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dag::potrf_dag_kernel, dim3(nwg), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+// Queue order of the persistent factorisation's tasks for a block of T tiles: tile tasks with
+// their dependencies, earliest start times from a critical-path pass (estimated µs: leaf 36,
+// strip task 4, hand-off 3), then Kahn's algorithm releasing the ready task of smallest start
+// time first (so the order is topological whatever the estimates), each tile task expanded into
+// its NP strips.  Word: type | part << 3 | i << 8 | j << 16 | k << 24.
+std::vector<uint32_t> dag_task_list(int T) {
+  struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0; };
+  std::vector<Task> tk;
+  std::vector<int> leaf(T), trsm(T * T, -1), fin(T * T, -1);
+  std::vector<int> upd_last(T * T, -1), updx_last(T * T, -1);
+  auto add = [&](int type, int i, int j, int k, std::vector<int> deps) {
+    Task t;
+    t.type = type; t.i = i; t.j = j; t.k = k;
+    for (int d : deps)
+      if (d >= 0) t.deps.push_back(d);
+    tk.push_back(t);
+    return (int)tk.size() - 1;
+  };
+  // factorisation, right-looking (generation order is topological)
+  for (int k = 0; k < T; ++k) {
+    leaf[k] = add(0, k, k, k, {upd_last[k * T + k]});
+    for (int i = k + 1; i < T; ++i) trsm[i * T + k] = add(1, i, k, k, {upd_last[i * T + k], leaf[k]});
+    for (int j = k + 1; j < T; ++j)
+      for (int i = j; i < T; ++i)
+        upd_last[i * T + j] = add(2, i, j, k, {trsm[i * T + k], trsm[j * T + k], upd_last[i * T + j]});
+  }
+  // inverse: X row j final → its terms pushed into every row i > j
+  auto xfinal = [&](int j, int k) { return j == k ? leaf[k] : fin[j * T + k]; };
+  for (int j = 0; j < T; ++j) {
+    for (int k = 0; k < j; ++k)  // X_jk = −X_jj S_jk once every term j' < j is in
+      fin[j * T + k] = add(4, j, k, k, {updx_last[j * T + k], leaf[j]});
+    for (int i = j + 1; i < T; ++i)
+      for (int k = 0; k <= j; ++k)
+        updx_last[i * T + k] = add(3, i, j, k, {trsm[i * T + j], xfinal(j, k), updx_last[i * T + k]});
+  }
+  const int n = (int)tk.size();
+  auto dur = [&](const Task& t) { return t.type == 0 ? 36.0 : 4.0; };
+  for (int t = 0; t < n; ++t)  // generation order is topological
+    for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
+  std::vector<std::vector<int>> succ(n);
+  std::vector<int> indeg(n, 0);
+  for (int t = 0; t < n; ++t)
+    for (int d : tk[t].deps) { succ[d].push_back(t); ++indeg[t]; }
+  std::priority_queue<std::pair<double, int>, std::vector<std::pair<double, int>>,
+                      std::greater<std::pair<double, int>>> ready;
+  for (int t = 0; t < n; ++t)
+    if (!indeg[t]) ready.push({tk[t].est, t});
+  std::vector<uint32_t> out;
+  while (!ready.empty()) {
+    const int t = ready.top().second;
+    ready.pop();
+    const Task& x = tk[t];
+    const int parts = x.type == 0 ? 1 : dag::NP;
+    for (int q = 0; q < parts; ++q)
+      out.push_back((uint32_t)x.type | (uint32_t)q << 3 | (uint32_t)x.i << 8 | (uint32_t)x.j << 16 |
+                    (uint32_t)x.k << 24);
+    for (int s2 : succ[t])
+      if (!--indeg[s2]) ready.push({tk[s2].est, s2});
+  }
+  return out;
+}
 
 hipError_t launch_potrf_leaf(const double* A, int64_t lda, double* Linv, int64_t ldl, double* Lout,
                              int64_t ldlo, double* logdiag, int* info, int base, int nreal,

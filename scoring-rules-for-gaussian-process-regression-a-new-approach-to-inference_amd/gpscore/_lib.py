@@ -20,6 +20,8 @@ GPS_FULL, GPS_LOWER = 0, 1
 GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
 GPS_OPT_GRAPH = 10
 GPS_OPT_PRED_PRE = 11
+GPS_OPT_DAG = 12
+GPS_OPT_DAG_TILES = 13
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
 GPS_SURF_LOGS_ADD_NOISE = 1
@@ -40,6 +42,7 @@ SIGNATURES = {
     "gps_ctx_synchronize": (_c_int, [_c_vp]),
     "gps_ctx_set_option": (_c_int, [_c_vp, _c_int, _c_int]),
     "gps_ctx_stats": (_c_int, [_c_vp, _c_vp]),
+    "gps_dag_task_list": (_c_int, [_c_int, _c_vp, _c_int]),
     "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
     "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
     "gps_gram": (_c_int, [_c_vp, _c_int, _P, _c_i64, _P, _c_i64, _c_int, _c_dbl, _P, _c_int,
@@ -188,6 +191,13 @@ class Context:
         """Replay the recursive factorisation from a captured hipGraph (default) or launch
         it eagerly."""
         self.call("gps_ctx_set_option", GPS_OPT_GRAPH, 1 if on else 0)
+
+    def set_dag(self, on=True, tiles=None):
+        """The persistent factorisation of the bottom diagonal blocks (GPS_OPT_DAG, default on)
+        and its largest block in 128-tiles (GPS_OPT_DAG_TILES)."""
+        self.call("gps_ctx_set_option", GPS_OPT_DAG, 1 if on else 0)
+        if tiles is not None:
+            self.call("gps_ctx_set_option", GPS_OPT_DAG_TILES, int(tiles))
 
     def set_pred_pre(self, on=True):
         """FITC: form the q_i = ||Lm^-1 k_i||^2 columns that need only the top-level Lm11^-1

@@ -1,0 +1,148 @@
+"""The persistent factorisation's task graph on CPU (no GPU): the queue libgpscore builds
+(gps_dag_task_list) replayed by a numpy emulator of the kernel's strip tasks and arrival
+counters (kernels_potrf.hip, dag::potrf_dag_kernel).
+
+* Every task's dependency counts are met when the queue is executed in order (the queue is a
+  topological order: a worker never waits on a task behind it, so the launch always drains).
+* Executing the strips in RANDOM orders allowed only by the counter thresholds (what the
+  device's workgroups may do under any timing) still gives L and L⁻¹ of the block: the
+  thresholds encode every true data dependency.
+Reference: torch.potrf KF:26 / KF:332, chol_solve(I, A) KF:242 — numpy.linalg here.
+"""
+import numpy as np
+import pytest
+
+NP_ = 4  # strips per tile task (dag::NP)
+B = 8    # emulated tile edge (the device uses 128; the algebra is edge-independent)
+
+
+def task_list(T):
+    import ctypes
+    from gpscore import _lib
+    lib = _lib.load()
+    n = lib.gps_dag_task_list(T, None, 0)
+    assert n > 0
+    out = (ctypes.c_uint32 * n)()
+    assert lib.gps_dag_task_list(T, ctypes.cast(out, ctypes.c_void_p), n) == n
+    return [(w & 7, (w >> 3) & 3, (w >> 8) & 255, (w >> 16) & 255, (w >> 24) & 255) for w in out]
+
+
+def needs(t, T):
+    """(counter array, i, j, threshold) pairs a strip task polls (the kernel's switch)."""
+    typ, _, i, j, k = t
+    if typ == 0:
+        return [("a", i, i, NP_ * i)]
+    if typ == 1:
+        return [("a", i, k, NP_ * k), ("a", k, k, NP_ * k + 1)]
+    if typ == 2:
+        return [("a", i, k, NP_ * (k + 1)), ("a", j, k, NP_ * (k + 1)), ("a", i, j, NP_ * k)]
+    if typ == 3:
+        return [("a", i, j, NP_ * (j + 1)), ("x", j, k, 1 if j == k else NP_ * (j - k + 1)),
+                ("x", i, k, NP_ * (j - k))]
+    return [("x", i, k, NP_ * (i - k)), ("x", i, i, 1)]
+
+
+class Emu:
+    """A (lower tiles, in place: L_ik lands in A_ik) and X (L⁻¹) of T×T tiles of edge B."""
+
+    def __init__(self, A, T):
+        self.T = T
+        self.A = A.copy()
+        self.X = np.full_like(A, np.nan)  # stale contents: every tile must be written first
+        self.cnt = {"a": np.zeros((T, T), int), "x": np.zeros((T, T), int)}
+
+    def ready(self, t):
+        return all(self.cnt[a][i, j] >= v for a, i, j, v in needs(t, self.T))
+
+    def blk(self, M, i, j):
+        return M[i * B:(i + 1) * B, j * B:(j + 1) * B]
+
+    def run(self, t):
+        typ, part, i, j, k = t
+        s = B // NP_  # strip width (32 of 128 on the device)
+        rows = slice(part * s, (part + 1) * s)
+        if typ == 0:  # LEAF(k = i): the leaf reads A_kk's lower triangle
+            L = np.linalg.cholesky(np.tril(self.blk(self.A, i, i)) + np.tril(self.blk(self.A, i, i), -1).T)
+            self.blk(self.X, i, i)[:] = np.linalg.inv(L)
+            self.cnt["a"][i, i] += 1
+            self.cnt["x"][i, i] += 1
+            return
+        if typ == 1:  # TRSM(i, k): row strip of L_ik = A_ik X_kkᵀ (in place)
+            C = self.blk(self.A, i, k)
+            C[rows] = C[rows] @ self.blk(self.X, k, k).T
+            self.cnt["a"][i, k] += 1
+        elif typ == 2:  # UPD(i, j, k): row strip of A_ij −= L_ik L_jkᵀ (diagonal: lower blocks)
+            C = self.blk(self.A, i, j)
+            upd = self.blk(self.A, i, k)[rows] @ self.blk(self.A, j, k).T
+            if i == j:  # waves right of the strip's diagonal block stay idle
+                upd[:, (part + 1) * s:] = 0.0
+            C[rows] -= upd
+            self.cnt["a"][i, j] += 1
+        elif typ == 3:  # UPDX(i, k, j): row strip of S_ik (+)= L_ij X_jk (first term overwrites)
+            C = self.blk(self.X, i, k)
+            prod = self.blk(self.A, i, j)[rows] @ self.blk(self.X, j, k)
+            C[rows] = prod if j == k else C[rows] + prod
+            self.cnt["x"][i, k] += 1
+        else:  # FIN(i, k): column strip of X_ik = −X_ii S_ik (in place)
+            C = self.blk(self.X, i, k)
+            C[:, rows] = -self.blk(self.X, i, i) @ C[:, rows]
+            self.cnt["x"][i, k] += 1
+
+
+def spd(T, seed):
+    rng = np.random.default_rng(seed)
+    M = rng.standard_normal((T * B, T * B))
+    return M @ M.T / (T * B) + np.eye(T * B)
+
+
+def check(em, A):
+    n = A.shape[0]
+    Lr = np.linalg.cholesky(A)
+    L = np.tril(em.A, -1) + np.zeros_like(A)
+    for t in range(em.T):  # diagonal tiles hold the updated A_kk; L_kk is the leaf's
+        blk = slice(t * B, (t + 1) * B)
+        L[blk, blk] = np.linalg.cholesky(np.tril(em.A[blk, blk]) + np.tril(em.A[blk, blk], -1).T)
+    X = np.where(np.tril(np.ones((n, n), bool)), em.X, 0.0)
+    assert np.allclose(L, Lr, rtol=1e-12, atol=1e-12)
+    assert np.allclose(X, np.linalg.inv(Lr), rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("T", [2, 3, 5, 8, 13])
+def test_queue_order_is_topological(T):
+    tl = task_list(T)
+    A = spd(T, T)
+    em = Emu(A, T)
+    for t in tl:
+        assert em.ready(t), t  # every input was produced by a task ahead in the queue
+        em.run(t)
+    check(em, A)
+    kinds = [t[0] for t in tl]
+    assert kinds.count(0) == T
+    assert kinds.count(1) == NP_ * T * (T - 1) // 2 and kinds.count(4) == NP_ * T * (T - 1) // 2
+
+
+@pytest.mark.parametrize("T,seed", [(4, 0), (6, 1), (9, 2)])
+def test_counters_cover_every_dependency(T, seed):
+    """Random execution orders permitted by the thresholds alone (any worker timing)."""
+    tl = task_list(T)
+    A = spd(T, 10 + seed)
+    em = Emu(A, T)
+    rng = np.random.default_rng(seed)
+    pending = list(tl)
+    while pending:
+        ready = [q for q, t in enumerate(pending) if em.ready(t)]
+        assert ready, "deadlock"
+        em.run(pending.pop(int(rng.choice(ready))))
+    check(em, A)
+
+
+def test_queue_sizes():
+    """Strip counts per block size (the device's ntasks) and the 64-tile limit."""
+    from gpscore import _lib
+    lib = _lib.load()
+    for T in (2, 20, 40):
+        n = lib.gps_dag_task_list(T, None, 0)
+        upd = T * (T - 1) * (T + 1) // 6          # Σ_k (T−1−k)(T−k)/2
+        updx = (T - 1) * T * (T + 1) // 6         # Σ_j (T−1−j)(j+1)
+        assert n == T + NP_ * (T * (T - 1) + upd + updx)
+    assert lib.gps_dag_task_list(65, None, 0) < 0 and lib.gps_dag_task_list(1, None, 0) < 0

@@ -576,7 +576,9 @@ def test_rccl_single_rank_comm(gpu_ctx):
             va, ga, oa = gpc.value_and_grad(th, o)
             vb, gb, ob = gpu.value_and_grad(th, o)
             assert abs(va - vb) <= 1e-13 * max(1, abs(vb)), o
-            assert nrel(ga, gb) <= 1e-12 and nrel(oa["grad_Z"], ob["grad_Z"]) <= 1e-12, o
+            # the packed all-reduce sums B in another order: the θ / Z gradients (one solve
+            # deeper than the forward) move by a few 1e-12 under that reordering
+            assert nrel(ga, gb) <= 1e-10 and nrel(oa["grad_Z"], ob["grad_Z"]) <= 1e-10, o
     finally:
         ctx.call("gps_comm_destroy")
         ctx.close()
@@ -635,3 +637,63 @@ def test_ctx_stats_graph_cache(gpu_ctx):
     assert s1["graph_cap"] == 256 and 1 <= s1["graphs"] <= s1["graph_cap"]
     assert s2["graphs"] == s1["graphs"] and s2["graph_overflow"] == s1["graph_overflow"]
     assert s1["device_bytes"] > 700 * 700 * 8
+
+
+@pytest.mark.parametrize("n,tiles", [(256, 20), (1000, 20), (2560, 20), (2561, 20), (5000, 20),
+                                     (3000, 2), (8192, 64), (4000, 40)])
+def test_persistent_factorisation_matches_recursion(gpu_ctx, n, tiles):
+    """GPS_OPT_DAG: the bottom diagonal blocks (≤ `tiles` 128-tiles; n = 8192 at 64 is one
+    persistent launch for the whole matrix) factored and inverted by the persistent task-queue
+    kernel against the recursion down to the 128-leaf — the same algorithm in another summation
+    order — and against the oracle; a refit is bitwise identical (fixed queue order, no
+    atomics in the arithmetic)."""
+    import gpscore
+    rng = np.random.default_rng(n + tiles)
+    d = 6
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((300, d))
+    y, yt = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n), np.sin(Xt.sum(1))
+    th = (0.2, np.log(1.7) * np.ones(d), np.log(0.02))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    runs = []
+    try:
+        for dag in (False, True, True):
+            gpu_ctx.set_dag(dag, tiles)
+            r = gp.fit(X, y, th)
+            mu, var = gp.predict(Xt, yt)
+            runs.append((r, mu, var))
+    finally:
+        gpu_ctx.set_dag(True, 20)
+    (r0, mu0, var0), (r1, mu1, var1), (r2, mu2, var2) = runs
+    assert r1.objectives == r2.objectives and np.array_equal(mu1, mu2) and np.array_equal(var2, var1)
+    assert np.array_equal(r1.mu_loo, r2.mu_loo) and np.array_equal(r1.var_loo, r2.var_loo)
+    for a, b in ((r1.mu_loo, r0.mu_loo), (r1.var_loo, r0.var_loo), (mu1, mu0), (var1, var0)):
+        assert nrel(a, b) < 1e-11
+    for k in ("nlml", "loo_crps", "loo_logs", "logdet", "quad"):
+        assert abs(r1.objectives[k] - r0.objectives[k]) <= 1e-11 * max(1.0, abs(r0.objectives[k])), k
+    f = O.fast_full_fit(X, y, *th)
+    assert nrel(r1.mu_loo, f["loo_mu"]) < 1e-9 and nrel(r1.var_loo, f["loo_var"]) < 1e-9
+    assert abs(r1.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
+
+
+def test_persistent_factorisation_potrf_exports(gpu_ctx):
+    """gps_potrf (L out of the persistent kernel's TRSM tasks and leaves) and the non-PD minor
+    reported from inside a persistent block."""
+    import gpscore
+    from gpscore import compat
+    from gpscore._lib import ptr
+    rng = np.random.default_rng(3)
+    n = 1900
+    M = rng.standard_normal((n, n)) / np.sqrt(n)
+    A = M @ M.T + 0.5 * np.eye(n)
+    L = A.copy()
+    ld = np.zeros(1)
+    gpu_ctx.call("gps_potrf", n, ptr(L), n, ptr(ld))
+    Lr = np.linalg.cholesky(A)
+    assert nrel(np.tril(L), Lr) < 1e-12
+    assert abs(ld[0] - 2 * np.sum(np.log(np.diag(Lr)))) < 1e-10 * n
+    assert nrel(compat.diag_inv(A), np.diag(np.linalg.inv(A))) < 1e-10
+    Abad = A.copy()
+    Abad[1500, 1500] = -5.0
+    with pytest.raises(gpscore.NotPositiveDefinite) as ei:
+        compat.half_logdet(Abad)
+    assert ei.value.info == 1501
