@@ -553,8 +553,20 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   int* acnt = p.cnt + 16;
   int* xcnt = acnt + T * T;
   int* err = p.info + 1;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Every branch that leaves the loop or spins is wave-uniform (readfirstlane): a loop exit the
+  // compiler must treat as divergent lets it rotate the `tid == 0` parts into another loop level
+  // than the rest of the wave, which then runs tasks without the lane that fetched them.
+  // The previous task's arrivals are published in the same lane-0 region that fetches the next
+  // task (one divergent region per iteration, right after the barrier that ends the task): two
+  // adjacent `tid == 0` regions around the loop latch get jump-threaded into a second back edge
+  // that only lane 0 takes, and the SIMT lowering then loops the other lanes over a stale task.
+  int* out = nullptr;
+  int* out2 = nullptr;
   for (;;) {
     if (tid == 0) {
+      if (out) __hip_atomic_fetch_add(out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (out2) __hip_atomic_fetch_add(out2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int t = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sh[0] = t < p.ntasks ? p.tasks[t] : 0xffffffffu;
       sh[1] = 0;
@@ -564,8 +576,9 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
     if (w == 0xffffffffu) break;
     const int type = w & 7, part = (w >> 3) & 3, ti = (w >> 8) & 255, tj = (w >> 16) & 255,
               tk = (w >> 24) & 255;
-    // ---- the counts this task needs (see the header); up to three
-    if (tid == 0) {
+    // ---- the counts this task needs (see the header); up to three, polled by wave 0 (every
+    //      lane loads the same word; the exit test is taken on lane 0's view)
+    if (wave == 0) {
       const int* c0 = nullptr; const int* c1 = nullptr; const int* c2 = nullptr;
       int v0 = 0, v1 = 0, v2 = 0;
       switch (type) {
@@ -591,33 +604,35 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
           c1 = xcnt + ti * T + ti; v1 = 1;
           break;
       }
+      if (!c1) { c1 = c0; v1 = v0; }
+      if (!c2) { c2 = c0; v2 = v0; }
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned int ab = 0;
       for (;;) {
-        bool ok = ld_cnt(c0) >= v0;
-        if (ok && c1) ok = ld_cnt(c1) >= v1;
-        if (ok && c2) ok = ld_cnt(c2) >= v2;
-        if (ok) break;
-        if (ld_cnt(err) != 0x7f7f7f7f) { sh[1] = 1; break; }
+        const int a0 = ld_cnt(c0), a1 = ld_cnt(c1), a2 = ld_cnt(c2), e = ld_cnt(err);
+        if (__builtin_amdgcn_readfirstlane((a0 >= v0 && a1 >= v1 && a2 >= v2) ? 1 : 0)) break;
+        if (__builtin_amdgcn_readfirstlane(e != 0x7f7f7f7f ? 1 : 0)) { ab = 1; break; }
         if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {  // a lost dependency
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          sh[1] = 1;
+          if (tid == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ab = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
       }
+      if (tid == 0) sh[1] = ab;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no loads above the poll
     }
     __syncthreads();
-    if (sh[1]) break;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (__builtin_amdgcn_readfirstlane(sh[1])) break;
     const int64_t lda = p.lda, ldl = p.ldl;
-    int* out = nullptr;
+    out2 = nullptr;
     if (type == 0) {
       const int64_t o = (int64_t)128 * ti;
       v4::leaf_body<true>(p.A + o * lda + o, lda, p.Linv + o * ldl + o, ldl,
                           p.Lout ? p.Lout + o * p.ldlo + o : nullptr, p.ldlo, p.logdiag + o,
                           p.info, p.base + (int)o, p.nreal - (int)o, S, DG);
       out = acnt + ti * T + ti;
+      out2 = xcnt + ti * T + ti;
     } else {
       Strip st;
       st.C2 = nullptr;
@@ -667,14 +682,10 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
       }
       run_strip(st);
     }
-    // ---- publish: every wave's write-through stores drained, then one arrival
+    // ---- publish: every wave's write-through stores drained, barrier; the arrival itself is
+    //      the first thing lane 0 does at the top of the next iteration
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_fetch_add(out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (type == 0)
-        __hip_atomic_fetch_add(xcnt + ti * T + ti, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 }  // namespace dag
