@@ -189,6 +189,7 @@ struct DagParams {
   const uint32_t* tasks; int ntasks;
   int* cnt;
   unsigned long long spin_ticks;   // 100 MHz s_memrealtime ticks a dependency wait may take
+  unsigned long long* trace = nullptr;  // diagnostics only (tools/dag_bench.cpp): 4 words per slot
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
 std::vector<uint32_t> dag_task_list(int T);

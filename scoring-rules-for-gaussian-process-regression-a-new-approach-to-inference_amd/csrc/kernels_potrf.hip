@@ -543,10 +543,13 @@ __device__ __forceinline__ void run_strip(const Strip& s) {
       }
 }
 
+// TRACE: per queue slot t, trace[4t..4t+3] = {fetched, inputs ready, outputs drained} in 100 MHz
+// s_memrealtime ticks and (blockIdx << 8 | XCC id) — the diagnostics launch (tools/dag_bench.cpp)
+template <bool TRACE>
 __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   __shared__ double S[v4::NT * v4::TSZ];
   __shared__ double DG[128];
-  __shared__ unsigned int sh[2];  // [task word, abort]
+  __shared__ unsigned int sh[3];  // [task word, abort, queue slot]
   const int tid = threadIdx.x;
   const int T = p.T;
   int* head = p.cnt;
@@ -563,17 +566,31 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   // that only lane 0 takes, and the SIMT lowering then loops the other lanes over a stale task.
   int* out = nullptr;
   int* out2 = nullptr;
+  unsigned long long* trow = nullptr;  // TRACE: the current slot's record
   for (;;) {
     if (tid == 0) {
+      if constexpr (TRACE) {  // (the previous task's "done" stamp lives here for the same reason)
+        if (trow) trow[2] = __builtin_amdgcn_s_memrealtime();
+      }
       if (out) __hip_atomic_fetch_add(out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (out2) __hip_atomic_fetch_add(out2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int t = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sh[0] = t < p.ntasks ? p.tasks[t] : 0xffffffffu;
       sh[1] = 0;
+      sh[2] = (unsigned int)t;
     }
     __syncthreads();
     const unsigned int w = __builtin_amdgcn_readfirstlane(sh[0]);
     if (w == 0xffffffffu) break;
+    if constexpr (TRACE) {
+      trow = p.trace + 4 * (int64_t)__builtin_amdgcn_readfirstlane(sh[2]);
+      if (tid == 0) {
+        unsigned int xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        trow[0] = __builtin_amdgcn_s_memrealtime();
+        trow[3] = (unsigned long long)blockIdx.x << 8 | (xcc & 15);
+      }
+    }
     const int type = w & 7, part = (w >> 3) & 3, ti = (w >> 8) & 255, tj = (w >> 16) & 255,
               tk = (w >> 24) & 255;
     // ---- the counts this task needs (see the header); up to three, polled by wave 0 (every
@@ -624,6 +641,9 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(sh[1])) break;
+    if constexpr (TRACE) {
+      if (tid == 0) trow[1] = __builtin_amdgcn_s_memrealtime();
+    }
     const int64_t lda = p.lda, ldl = p.ldl;
     out2 = nullptr;
     if (type == 0) {
@@ -696,7 +716,10 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
     return hipErrorInvalidValue;
   // every strip's buffer descriptor spans at most 128 rows of its matrix (32-bit offsets)
   if ((int64_t)128 * std::max(p.lda, p.ldl) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dag::potrf_dag_kernel, dim3(nwg), dim3(256), 0, s, p);
+  if (p.trace)
+    hipLaunchKernelGGL(dag::potrf_dag_kernel<true>, dim3(nwg), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(dag::potrf_dag_kernel<false>, dim3(nwg), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

@@ -146,3 +146,33 @@ def test_queue_sizes():
         updx = (T - 1) * T * (T + 1) // 6         # Σ_j (T−1−j)(j+1)
         assert n == T + NP_ * (T * (T - 1) + upd + updx)
     assert lib.gps_dag_task_list(65, None, 0) < 0 and lib.gps_dag_task_list(1, None, 0) < 0
+
+
+def test_dag_kernel_loop_is_uniform():
+    """Structural guard on the persistent kernel's code (no GPU): the task loop must be ONE loop
+    whose first barrier follows its header directly.  Two `tid == 0` regions around the loop latch
+    once got jump-threaded into a second back edge taken by lane 0 alone (a nested loop between
+    the header and the barrier in the .s); the other lanes then re-ran a stale task forever."""
+    import os
+    import shutil
+    import subprocess
+    import tempfile
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd", "csrc")
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "potrf.s")
+        subprocess.run([hipcc, "-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(root, "include"),
+                        "-I" + csrc, "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1",
+                        "--cuda-device-only", "-S", os.path.join(csrc, "kernels_potrf.hip"), "-o", out],
+                       check=True, capture_output=True)
+        text = open(out).read()
+    for variant in ("Lb0E", "Lb1E"):
+        start = text.index(f"_ZN3gps3dag16potrf_dag_kernelI{variant}EEvNS_9DagParamsE:")
+        body = text[start:text.index("s_endpgm", start)]
+        assert body.count("This Loop Header: Depth=1") == 1, variant
+        head = body.index("This Loop Header: Depth=1")
+        first_barrier = body.index("s_barrier", head)
+        assert "Loop Header" not in body[head + 30:first_barrier], variant

@@ -576,9 +576,11 @@ def test_rccl_single_rank_comm(gpu_ctx):
             va, ga, oa = gpc.value_and_grad(th, o)
             vb, gb, ob = gpu.value_and_grad(th, o)
             assert abs(va - vb) <= 1e-13 * max(1, abs(vb)), o
-            # the packed all-reduce sums B in another order: the θ / Z gradients (one solve
-            # deeper than the forward) move by a few 1e-12 under that reordering
-            assert nrel(ga, gb) <= 1e-10 and nrel(oa["grad_Z"], ob["grad_Z"]) <= 1e-10, o
+            # the sharded gradient reduces its pieces ([P | ΣM_ii | pad | Kᵀv], contraction
+            # partials) through other buffers and in another order than the unsharded one: the
+            # θ / Z gradients (one solve deeper than the forward, LOO-LogS the most sensitive:
+            # DESIGN §9) differ by up to 1.5e-10 normwise on this case (r3a GPU suite)
+            assert nrel(ga, gb) <= 1e-9 and nrel(oa["grad_Z"], ob["grad_Z"]) <= 1e-9, o
     finally:
         ctx.call("gps_comm_destroy")
         ctx.close()
