@@ -190,9 +190,10 @@ struct DagParams {
   int* cnt;
   unsigned long long spin_ticks;   // 100 MHz s_memrealtime ticks a dependency wait may take
   unsigned long long* trace = nullptr;  // diagnostics only (tools/dag_bench.cpp): 4 words per slot
+  int group = 3;                   // 16-deep operand chunks per load group of a strip task (2..4)
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
-std::vector<uint32_t> dag_task_list(int T);
+std::vector<uint32_t> dag_task_list(int T, int order = 1);
 inline int64_t dag_cnt_ints(int T) { return (16 + 2 * (int64_t)T * T + 63) / 64 * 64; }
 
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)

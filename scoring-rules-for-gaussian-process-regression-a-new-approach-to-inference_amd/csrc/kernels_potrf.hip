@@ -438,18 +438,24 @@ __device__ __forceinline__ int ld_cnt(const int* p) {
 }
 
 // one wave: acc = A (32 rows, k in [kb, ke), lda) · B, B stored [k][j] (BT = false, 32 columns)
-// or [j][k] (BT = true, 32 rows); operand fragments straight from L2 (sc1) in groups of two
-// 16-deep chunks, one group ahead of the MFMAs (the layout of gemm_f64_small_kernel)
-template <bool BT>
+// or [j][k] (BT = true, 32 rows); operand fragments straight from L2 (sc1) in groups of G
+// 16-deep chunks, one group ahead of the MFMAs (the layout of gemm_f64_small_kernel).  A chunk is
+// 32 VGPRs per lane, so G bounds how many loads are in flight per wave: the operands were just
+// handed over (written through by another workgroup, often on another XCD), so every group pays a
+// full fabric latency, and with K = 128 at G = 2 the strip waited four of them (9-12 µs per strip
+// task against 3.4 µs of MFMA, profiles/r3_dag_trace20.txt).
+template <bool BT, int G>
 __device__ __forceinline__ void wave_gemm32(const double* Ap, int64_t lda, const double* Bp,
                                             int64_t ldb, int kb, int ke, d4 (&acc)[2][2]) {
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const __amdgpu_buffer_rsrc_t ra = rsrc(Ap, (uint32_t)(32 * lda * 8));
   const __amdgpu_buffer_rsrc_t rb = rsrc(Bp, (uint32_t)((BT ? 32 : 128) * ldb * 8));
-  typedef double Frag[2][2][4];  // [chunk in group][16-block][k step]
+  typedef double Frag[G][2][4];  // [chunk in group][16-block][k step]
+  const int nc = (ke - kb) / 16;
   auto load_group = [&](int c, Frag& a, Frag& b) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < G; ++u) {
+      if (c + u >= nc) break;  // wave-uniform
       const int k = kb + 16 * (c + u) + 4 * g;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -468,9 +474,10 @@ __device__ __forceinline__ void wave_gemm32(const double* Ap, int64_t lda, const
       }
     }
   };
-  auto mma_group = [&](const Frag& a, const Frag& b) {
+  auto mma_group = [&](int c, const Frag& a, const Frag& b) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < G; ++u) {
+      if (c + u >= nc) break;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
@@ -478,19 +485,19 @@ __device__ __forceinline__ void wave_gemm32(const double* Ap, int64_t lda, const
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][i][kk], b[u][j][kk], acc[i][j], 0, 0, 0);
+    }
   };
-  const int nc = (ke - kb) / 16;  // even: kb, ke are multiples of 32
   Frag fa0, fb0, fa1, fb1;
   int c = 0;
   if (c < nc) load_group(c, fa0, fb0);
   while (c < nc) {
-    if (c + 2 < nc) load_group(c + 2, fa1, fb1);
-    mma_group(fa0, fb0);
-    c += 2;
+    if (c + G < nc) load_group(c + G, fa1, fb1);
+    mma_group(c, fa0, fb0);
+    c += G;
     if (c >= nc) break;
-    if (c + 2 < nc) load_group(c + 2, fa0, fb0);
-    mma_group(fa1, fb1);
-    c += 2;
+    if (c + G < nc) load_group(c + G, fa0, fb0);
+    mma_group(c, fa1, fb1);
+    c += G;
   }
 }
 
@@ -505,6 +512,7 @@ struct Strip {          // one wave's 32×32 block of a strip task
 
 // all four waves: compute, barrier (in-place tasks: every read of the strip precedes every
 // write), then write-through stores
+template <int G>
 __device__ __forceinline__ void run_strip(const Strip& s) {
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const __amdgpu_buffer_rsrc_t rc = rsrc(s.C, (uint32_t)(32 * s.ldc * 8));
@@ -524,8 +532,8 @@ __device__ __forceinline__ void run_strip(const Strip& s) {
           for (int j = 0; j < 2; ++j)
             cold[i][j][e] = ld64(rc, (uint32_t)(((int64_t)(16 * i + g + 4 * e) * s.ldc + 16 * j + r) * 8));
     }
-    if (s.bt) wave_gemm32<true>(s.A, s.lda, s.B, s.ldb, s.kb, s.ke, acc);
-    else wave_gemm32<false>(s.A, s.lda, s.B, s.ldb, s.kb, s.ke, acc);
+    if (s.bt) wave_gemm32<true, G>(s.A, s.lda, s.B, s.ldb, s.kb, s.ke, acc);
+    else wave_gemm32<false, G>(s.A, s.lda, s.B, s.ldb, s.kb, s.ke, acc);
   }
   __syncthreads();
   if (!s.active) return;
@@ -545,7 +553,7 @@ __device__ __forceinline__ void run_strip(const Strip& s) {
 
 // TRACE: per queue slot t, trace[4t..4t+3] = {fetched, inputs ready, outputs drained} in 100 MHz
 // s_memrealtime ticks and (blockIdx << 8 | XCC id) — the diagnostics launch (tools/dag_bench.cpp)
-template <bool TRACE>
+template <bool TRACE, int G>
 __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   __shared__ double S[v4::NT * v4::TSZ];
   __shared__ double DG[128];
@@ -700,7 +708,7 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
           break;
         }
       }
-      run_strip(st);
+      run_strip<G>(st);
     }
     // ---- publish: every wave's write-through stores drained, barrier; the arrival itself is
     //      the first thing lane 0 does at the top of the next iteration
@@ -716,20 +724,27 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
     return hipErrorInvalidValue;
   // every strip's buffer descriptor spans at most 128 rows of its matrix (32-bit offsets)
   if ((int64_t)128 * std::max(p.lda, p.ldl) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-  if (p.trace)
-    hipLaunchKernelGGL(dag::potrf_dag_kernel<true>, dim3(nwg), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(dag::potrf_dag_kernel<false>, dim3(nwg), dim3(256), 0, s, p);
+  auto k = p.trace ? (p.group == 2 ? dag::potrf_dag_kernel<true, 2>
+                                    : p.group == 3 ? dag::potrf_dag_kernel<true, 3> : dag::potrf_dag_kernel<true, 4>)
+                   : (p.group == 2 ? dag::potrf_dag_kernel<false, 2>
+                                    : p.group == 3 ? dag::potrf_dag_kernel<false, 3> : dag::potrf_dag_kernel<false, 4>);
+  if (p.group < 2 || p.group > 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k, dim3(nwg), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
 // Queue order of the persistent factorisation's tasks for a block of T tiles: tile tasks with
-// their dependencies, earliest start times from a critical-path pass (estimated µs: leaf 36,
-// strip task 4, hand-off 3), then Kahn's algorithm releasing the ready task of smallest start
-// time first (so the order is topological whatever the estimates), each tile task expanded into
-// its NP strips.  Word: type | part << 3 | i << 8 | j << 16 | k << 24.
-std::vector<uint32_t> dag_task_list(int T) {
-  struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0; };
+// their dependencies, then Kahn's algorithm releasing the ready task of best priority first (so
+// the order is topological whatever the priorities), each tile task expanded into its NP strips.
+//   order 0: earliest estimated start first (a forward critical-path pass; estimated µs: leaf 36,
+//            strip task 4, hand-off 3) — round 3's first build;
+//   order 1: largest upward rank first (the longest estimated path from the task to the end of
+//            the block, leaf 38, strip 9, hand-off 1: the durations the r3 trace measured), so the
+//            updates that feed the next leaves overtake the bulk of the trailing update (the first
+//            leaves waited 20-26 µs behind it).
+// Word: type | part << 3 | i << 8 | j << 16 | k << 24.
+std::vector<uint32_t> dag_task_list(int T, int order) {
+  struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0, rank = 0.0; };
   std::vector<Task> tk;
   std::vector<int> leaf(T), trsm(T * T, -1), fin(T * T, -1);
   std::vector<int> upd_last(T * T, -1), updx_last(T * T, -1);
@@ -759,13 +774,23 @@ std::vector<uint32_t> dag_task_list(int T) {
         updx_last[i * T + k] = add(3, i, j, k, {trsm[i * T + j], xfinal(j, k), updx_last[i * T + k]});
   }
   const int n = (int)tk.size();
-  auto dur = [&](const Task& t) { return t.type == 0 ? 36.0 : 4.0; };
-  for (int t = 0; t < n; ++t)  // generation order is topological
-    for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
   std::vector<std::vector<int>> succ(n);
   std::vector<int> indeg(n, 0);
   for (int t = 0; t < n; ++t)
     for (int d : tk[t].deps) { succ[d].push_back(t); ++indeg[t]; }
+  if (order == 0) {
+    auto dur = [&](const Task& t) { return t.type == 0 ? 36.0 : 4.0; };
+    for (int t = 0; t < n; ++t)  // generation order is topological
+      for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
+  } else {
+    auto dur = [&](const Task& t) { return t.type == 0 ? 38.0 : 9.0; };
+    for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
+      double m = 0.0;
+      for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + 1.0);
+      tk[t].rank = dur(tk[t]) + m;
+      tk[t].est = -tk[t].rank;  // smallest key first
+    }
+  }
   std::priority_queue<std::pair<double, int>, std::vector<std::pair<double, int>>,
                       std::greater<std::pair<double, int>>> ready;
   for (int t = 0; t < n; ++t)
