@@ -91,6 +91,14 @@ enum {
                             inverted by ONE persistent launch (a device task queue of tile
                             products, per-tile arrival counters); 0: the recursion down to
                             the 128-block leaf.  Same algorithm, other summation order. */
+  GPS_OPT_FORK_MAX = 14, /* largest recursion block (in 128-row blocks) whose off-critical-path
+                            product is forked; 0 (default): no limit */
+  GPS_OPT_AR_CHUNKS = 15, /* sharded FITC: B's all-reduce in this many row blocks (default 4),
+                             each on a comm stream while the next block's SYRK runs; 1: one
+                             all-reduce after the SYRK.  Same bits either way. */
+  GPS_OPT_SIDE_PRIO = 16, /* 1: the side stream (the factorisation's T products) at the lowest
+                             queue priority, so the main stream's launches are dispatched first
+                             as workgroup slots free up; 0 (default): equal priority */
   GPS_OPT_DAG_TILES = 13, /* largest block (in 128-tiles, 2..64, default 20) the persistent
                             factorisation takes */
 };

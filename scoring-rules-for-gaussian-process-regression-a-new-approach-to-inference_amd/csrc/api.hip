@@ -90,6 +90,10 @@ struct gps_ctx {
   bool overlap = true;                 // GPS_OPT_OVERLAP
   int gemm_map = 0;                    // GPS_OPT_GEMM_MAP: tile-order override (A/B measurements)
   int fork_min = 1;                    // GPS_OPT_FORK_MIN: smallest n1 (in 128-blocks) whose T GEMM
+  int fork_max = 0;                    // GPS_OPT_FORK_MAX: largest such n1 (0: no limit)
+  bool side_low = false;               // GPS_OPT_SIDE_PRIO: side stream at the lowest priority
+  int ar_chunks = 4;                   // GPS_OPT_AR_CHUNKS: row blocks of the FITC B all-reduce
+  std::vector<hipEvent_t> ar_ev;       // their hand-offs to the comm stream (aux[1])
                                        // goes to the side stream (a fork/join costs ~13 us, but
                                        // forking every level measured best: 128.3 vs 129.1 ms)
   int ncu = 0;
@@ -449,7 +453,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
                                     (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
   // an event fork + join costs ~13 us of dependent-chain latency (tools/launch_latency.hip)
-  const bool forked = ctx->overlap && n1b >= ctx->fork_min;
+  const bool forked = ctx->overlap && n1b >= ctx->fork_min && (!ctx->fork_max || n1b <= ctx->fork_max);
   hipStream_t ts = forked ? ctx->side : s;
   hipEvent_t fork = sync_event(ctx), join = sync_event(ctx);
   if (!fork || !join) return fail(ctx, -2, "hipEventCreate failed");
@@ -530,8 +534,13 @@ constexpr size_t kMaxGraphs = 256;
 
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
-  // persistent blocks: task lists per size (uploaded once, before any capture) and one zeroed
-  // counter region per launch of this call (a memset node ahead of the sequence)
+  // persistent blocks: task lists per size (uploaded once, before any capture) and one counter
+  // region per launch of this call.  The regions are zero when a launch starts: zeroed once when
+  // the buffer is allocated (synchronously, outside any capture) and reset by each launch's last
+  // workgroup on its way out, so the captured sequence holds kernel nodes only.  (A memset node
+  // ahead of the sequence, the first design, was replayed with garbage in the counters after
+  // ~60 other captures on the GPU suite's context: pointer-valued words in the head counter,
+  // then a no-op or a dependency wait that timed out; the r3 suite runs 3c-3e.)
   std::vector<int> dsizes;
   int64_t dcnt = 0;
   dag_blocks(ctx, n_pad / GPS_TILE, dsizes, dcnt);
@@ -543,24 +552,29 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
     HIPCHK(hipMemcpy(e.first.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice));
     e.second = (int)tl.size();
   }
-  if (dcnt) HIPCHK(ensure(ctx->dag_cnt, (size_t)dcnt * 4));
+  if (dcnt && ctx->dag_cnt.cap < (size_t)dcnt * 4) {
+    HIPCHK(hipStreamSynchronize(ctx->stream));  // no launch of this context still uses the old one
+    HIPCHK(ensure(ctx->dag_cnt, std::max<size_t>((size_t)dcnt * 4, (size_t)1 << 20)));
+    HIPCHK(hipMemset(ctx->dag_cnt.p, 0, ctx->dag_cnt.cap));
+    HIPCHK(hipDeviceSynchronize());
+  }
   auto eager = [&]() {
     ctx->sync_used = 0;
     ctx->pre.join = nullptr;
     ctx->dag_cnt_used = 0;
-    if (dcnt) {
-      hipError_t e = hipMemsetAsync(ctx->dag_cnt.p, 0, (size_t)dcnt * 4, ctx->stream);
-      if (e != hipSuccess) return fail(ctx, -2, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
-    }
     return potrf_inv_rec(ctx, A, n_pad, Linv, n_pad, W, (int)(n_pad / GPS_TILE), logdiag,
                          static_cast<int*>(ctx->info.p), 0, nreal, Lout, n_pad, true);
   };
   if (!ctx->graphs || ctx->prof || n_pad <= GPS_TILE) return eager();
+  // capture: everything the recursion allocates must exist beforehand (no allocation inside a
+  // capture), and the key names the buffers the sequence bakes in: the split-K workspaces first
+  HIPCHK(ensure(ctx->ws_main, (size_t)kSplitWsDoubles * 8));
+  HIPCHK(ensure(ctx->ws_side, (size_t)kSplitWsDoubles * 8));
   const bool pre = ctx->pre.kind == PRE_FITC_Q;
   const std::vector<uintptr_t> key = {
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
-      (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->gemm_map,
+      (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->fork_max, (uintptr_t)ctx->gemm_map,
       (uintptr_t)g_tiny_gemm, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
       (uintptr_t)ctx->ws_side.p, (uintptr_t)pre,
       // the pre-pass's operands (only when it is part of the sequence)
@@ -582,18 +596,13 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
     ++ctx->graph_overflow;
     return eager();
   }
-  // capture: everything the recursion allocates must exist beforehand (no allocation
-  // inside a capture): the split-K workspaces and the fork/join event pool
-  HIPCHK(ensure(ctx->ws_main, (size_t)kSplitWsDoubles * 8));
-  HIPCHK(ensure(ctx->ws_side, (size_t)kSplitWsDoubles * 8));
+  // ... and the fork/join event pool
   const size_t nev = 2 * (size_t)(n_pad / GPS_TILE) + 8;
   while (ctx->sync_ev.size() < nev) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ctx->sync_ev.push_back(e);
   }
-  if (key[14] != (uintptr_t)ctx->ws_main.p || key[15] != (uintptr_t)ctx->ws_side.p)
-    return potrf_inv(ctx, A, n_pad, Linv, W, logdiag, nreal, Lout);  // key with the new buffers
   HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
   int rc = eager();
   hipGraph_t graph = nullptr;
@@ -1154,6 +1163,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (auto& kv : ctx->dag_lists) release(kv.second.first);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join})
     if (e) (void)hipEventDestroy(e);
   for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
@@ -1189,6 +1199,23 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
     case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
+    case GPS_OPT_FORK_MAX: ctx->fork_max = value < 0 ? 0 : value; return 0;
+    case GPS_OPT_SIDE_PRIO: {  // the side stream at the lowest queue priority (or back)
+      if ((value != 0) == ctx->side_low) return 0;
+      int least = 0, greatest = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIPCHK(hipStreamSynchronize(ctx->side));
+      HIPCHK(hipStreamDestroy(ctx->side));
+      ctx->side = nullptr;
+      if (value) HIPCHK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
+      else HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+      ctx->side_low = value != 0;
+      return 0;
+    }
+    case GPS_OPT_AR_CHUNKS:
+      ARGCHK(value >= 1 && value <= 64, "GPS_OPT_AR_CHUNKS must be in 1..64");
+      ctx->ar_chunks = value;
+      return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
@@ -1721,8 +1748,7 @@ int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m) {
 // -> 95 %), with at least 1024 rows per slice and at most 32 slabs.
 // With `packed` the sum goes lower-packed (m(m+1)/2, launch_sym_pack) into dst instead: the
 // all-reduce payload of the row-sharded path (base must be NULL then).
-int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* dst,
-              bool packed = false) {
+int fitc_syrk_ks(const gps_ctx* ctx) {
   const int64_t np = ctx->fn_pad, mp = ctx->m_pad, tm = mp / GPS_TILE;
   const int64_t tiles_lower = tm * (tm + 1) / 2;
   int ks = 1;
@@ -1734,19 +1760,100 @@ int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* ds
   // and slices of at most ~8k rows: at n = 200k (C5) 24 slices ran 1 % faster than the 12 the
   // fill rule gives (more workgroups share each slice's rows through the Infinity Cache), at
   // n = 40k (C4) more slices than the fill rule's 11 were slower (profiles/r2_syrk_ks_ab.txt)
-  ks = (int)std::max<int64_t>(ks, std::min<int64_t>(32, (np + 8191) / 8192));
+  return (int)std::max<int64_t>(ks, std::min<int64_t>(32, (np + 8191) / 8192));
+}
+
+// split-K SYRK slabs of B's rows [R0, R1) (128-aligned): the rectangle left of the diagonal
+// block and the diagonal block's lower tiles, K slices as the whole-matrix launch would cut them
+// (same ks, same per-tile K ranges), so a row block's slab values are bitwise those of the
+// unchunked SYRK
+int fitc_syrk_rows(gps_ctx* ctx, const double* kscale, int ks, int64_t R0, int64_t R1) {
+  const int64_t np = ctx->fn_pad, mp = ctx->m_pad;
+  double* slab = ctx->slabB.d();
+  if (R0 > 0) {
+    GemmParams p = gp0();
+    p.A = ctx->Knm.d() + R0; p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
+    p.C = slab + R0 * mp; p.ldc = mp; p.c_kslice_stride = mp * mp;
+    p.M = (int)(R1 - R0); p.N = (int)R0; p.K = (int)np; p.kscale = kscale; p.ksplit = ks;
+    if (int rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p)) return rc;
+  }
+  GemmParams p = gp0();
+  p.A = ctx->Knm.d() + R0; p.lda = mp; p.B = ctx->Knm.d() + R0; p.ldb = mp;
+  p.C = slab + R0 * mp + R0; p.ldc = mp; p.c_kslice_stride = mp * mp;
+  p.M = (int)(R1 - R0); p.N = (int)(R1 - R0); p.K = (int)np; p.kscale = kscale;
+  p.lower_out = 1; p.ksplit = ks;
+  return gemm(ctx, LAY_T, LAY_N, EPI_STORE, p);
+}
+
+// B_p = Kmnᵀ diag(kscale) Knm over this rank's rows (K20:222-234's big_Q restated as the
+// Woodbury m×m form), split-K slabs summed in fixed order; base (if given) added; dst = the
+// padded lower tiles.  With `packed` the sum goes lower-packed (m(m+1)/2, launch_sym_pack) into
+// dst instead: the payload of the ranks' all-reduce.
+int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* dst,
+              bool packed = false) {
+  const int64_t mp = ctx->m_pad;
+  const int ks = fitc_syrk_ks(ctx);
   HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
   GemmParams p = gp0();
   p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
   p.C = ctx->slabB.d(); p.ldc = mp; p.c_kslice_stride = mp * mp;
-  p.M = (int)mp; p.N = (int)mp; p.K = (int)np; p.kscale = kscale;
+  p.M = (int)mp; p.N = (int)mp; p.K = (int)ctx->fn_pad; p.kscale = kscale;
   p.lower_out = 1; p.ksplit = ks;
   if (int rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p)) return rc;
   Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * mp * mp);
   if (packed)
-    HIPCHK(launch_sym_pack(ctx->slabB.d(), mp * mp, ks, (int)ctx->m, (int)mp, dst, ctx->stream));
+    HIPCHK(launch_sym_pack(ctx->slabB.d(), mp * mp, ks, 0, (int)ctx->m, (int)mp, dst, ctx->stream));
   else
     HIPCHK(launch_sym_slab_sum(ctx->slabB.d(), mp * mp, ks, (int)mp, base, dst, ctx->stream));
+  return 0;
+}
+
+// The sharded forward's exchange: B_p lower-packed, then [b | Σlogλ | Σy²/λ],
+// summed over the ranks.  With ctx->ar_chunks > 1 B's rows go in blocks of about equal packed
+// size: block c's slabs are formed and packed on the main stream, then all-reduced on the comm
+// stream (aux[1]) while block c+1's SYRK runs; the last block carries b and the scalars, and
+// the main stream waits for the comm stream before unpacking.  Chunked and unchunked give the
+// same bits (the slab values do not depend on the row blocks; tests/test_gpu_shards.py).
+int fitc_syrk_allreduce(gps_ctx* ctx, double* red, int64_t blen, int64_t tail) {
+  const int64_t m = ctx->m, mp = ctx->m_pad, tm = mp / GPS_TILE;
+  hipStream_t s = ctx->stream;
+  const int nch = (int)std::min<int64_t>(std::max(1, ctx->ar_chunks), tm);
+  if (nch <= 1) {
+    if (int rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, red, true)) return rc;
+    Prof pr(ctx, "allreduce_B", 0, 8.0 * (blen + tail));
+    return allreduce_sum(ctx, red, (size_t)(blen + tail), s);
+  }
+  const int ks = fitc_syrk_ks(ctx);
+  HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
+  hipStream_t cs = ctx->aux[1];
+  while ((int)ctx->ar_ev.size() < nch + 1) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->ar_ev.push_back(e);
+  }
+  int64_t R0 = 0;
+  for (int c = 0; c < nch; ++c) {
+    // row-block ends at equal packed sizes: R_c = m·sqrt(c/nch), 128-aligned, strictly growing
+    int64_t R1 = c + 1 == nch ? mp
+                              : (int64_t)std::llround(std::sqrt((double)(c + 1) / nch) * (double)tm) * GPS_TILE;
+    R1 = std::min<int64_t>(std::max<int64_t>(R1, R0 + GPS_TILE), mp - (int64_t)(nch - 1 - c) * GPS_TILE);
+    if (int rc = fitc_syrk_rows(ctx, ctx->ilam.d(), ks, R0, R1)) return rc;
+    const int r0 = (int)std::min<int64_t>(R0, m), r1 = (int)std::min<int64_t>(R1, m);
+    {
+      Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * (R1 - R0) * R1);
+      HIPCHK(launch_sym_pack(ctx->slabB.d(), mp * mp, ks, r0, r1, (int)mp, red, s));
+    }
+    HIPCHK(hipEventRecord(ctx->ar_ev[c], s));
+    HIPCHK(hipStreamWaitEvent(cs, ctx->ar_ev[c], 0));
+    const int64_t e0 = (int64_t)r0 * (r0 + 1) / 2;
+    const int64_t e1 = c + 1 == nch ? blen + tail : (int64_t)r1 * (r1 + 1) / 2;
+    Prof pr(ctx, "allreduce_B", 0, 8.0 * (e1 - e0), cs);
+    if (e1 > e0)
+      if (int rc = allreduce_sum(ctx, red + e0, (size_t)(e1 - e0), cs)) return rc;
+    R0 = R1;
+  }
+  HIPCHK(hipEventRecord(ctx->ar_ev[nch], cs));
+  HIPCHK(hipStreamWaitEvent(s, ctx->ar_ev[nch], 0));
   return 0;
 }
 
@@ -1861,16 +1968,17 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     HIPCHK(launch_fitc_lambda(ctx->q.d(), ctx->fy.d(), (int)n, (int)np, th.sf2, th.sn2,
                               ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal, s));
   }
-  // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs)
-  if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc, shard))) return rc;
   {  // b_p = Kmnᵀ Λ⁻¹ y
     Prof pr(ctx, "colred_b", 0, 8.0 * np * mp);
     HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ctx->ys.d(), nullptr, bvec,
                          nullptr, ctx->fslab.d(), s));
   }
-  if (shard) {  // ONE all-reduce: B packed, b, Σlogλ, Σy²/λ
-    Prof pr(ctx, "allreduce_B", 0, 8.0 * (blen + mp + 2));
-    if ((rc = allreduce_sum(ctx, red, (size_t)(blen + mp + 2), s))) return rc;
+  // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs); sharded: packed and all-reduced with b,
+  // Σlogλ, Σy²/λ, in row blocks overlapped with the SYRK (ctx->ar_chunks)
+  if (shard) {
+    if ((rc = fitc_syrk_allreduce(ctx, red, blen, mp + 2))) return rc;
+  } else if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc, false))) {
+    return rc;
   }
   if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
     if ((rc = fitc_test_prepass(ctx))) return rc;

@@ -178,8 +178,8 @@ hipError_t launch_potrf_leaf(const double* A, int64_t lda, double* Linv, int64_t
 
 // persistent tiled factorisation of a diagonal block of T tiles (kernels_potrf.hip): L⁻¹ into
 // Linv, L into A's strictly-lower tiles (and Lout if given), logdiag, info[0] as the leaf;
-// info[1] != 0x7f7f7f7f on a lost dependency (bounded spin).  cnt: 16 + 2·T² ints, zeroed
-// before the launch; tasks: dag_task_list(T) on the device.
+// info[1] != 0x7f7f7f7f on a lost dependency (bounded spin).  cnt: 16 + 2·T² ints, zero at the
+// launch and left zero by it (its last workgroup resets them); tasks: dag_task_list(T) on the device.
 struct DagParams {
   double* A; int64_t lda;
   double* Linv; int64_t ldl;
@@ -217,10 +217,10 @@ hipError_t launch_sym_slab_sum(const double* slab, int64_t slice_stride, int nsl
                                const double* base, double* dst, hipStream_t s);
 
 // symmetric m×m accumulator <-> lower-packed m(m+1)/2 (the FITC all-reduce payload):
-// packed = Σ_q slab_q (lower, row-major);  dst (M×M) = base + unpack(packed), lower 128-tiles
-// (strict-upper tiles zero) or, with full, both triangles
-hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, int m, int M,
-                           double* packed, hipStream_t s);
+// packed = Σ_q slab_q (lower, row-major; rows [r0, r1) only);  dst (M×M) = base +
+// unpack(packed), lower 128-tiles (strict-upper tiles zero) or, with full, both triangles
+hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, int r0, int r1,
+                           int M, double* packed, hipStream_t s);
 hipError_t launch_sym_unpack(const double* packed, int m, int M, const double* base, int full,
                              double* dst, hipStream_t s);
 // full-GP LOO finalize (one workgroup): see kernels_vec.hip

@@ -551,6 +551,8 @@ __device__ __forceinline__ void run_strip(const Strip& s) {
       }
 }
 
+// Counters: cnt[0] the queue head, cnt[1] the workgroups out, cnt[16..] the arrival counters —
+// zero at launch, zero again when the last workgroup leaves.
 // TRACE: per queue slot t, trace[4t..4t+3] = {fetched, inputs ready, outputs drained} in 100 MHz
 // s_memrealtime ticks and (blockIdx << 8 | XCC id) — the diagnostics launch (tools/dag_bench.cpp)
 template <bool TRACE, int G>
@@ -714,6 +716,21 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
     //      the first thing lane 0 does at the top of the next iteration
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  // ---- the last workgroup out zeroes this launch's counters for the next launch (no memset node
+  //      ahead of a replayed sequence).  Every workgroup first waits for its own counter atomics
+  //      (the last arrival has no return value; vmcnt covers it), then counts itself out.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int e = __hip_atomic_fetch_add(p.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[1] = e == (int)gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(sh[1])) {
+    const int n = 16 + 2 * T * T;
+    for (int i = tid; i < n; i += 256)
+      __hip_atomic_store(p.cnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 }  // namespace dag

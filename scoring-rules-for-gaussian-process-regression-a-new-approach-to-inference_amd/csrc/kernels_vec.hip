@@ -145,12 +145,14 @@ hipError_t launch_sym_slab_sum(const double* slab, int64_t slice_stride, int nsl
 // the padded m_pad².  Pack sums the split-K slabs in slice order (the
 // same sums sym_slab_sum forms); unpack adds the optional base and writes either the
 // lower 128-tiles (strict-upper tiles zero, as sym_slab_sum) or the full symmetric matrix.
+// packed elements [e0, e1) of the lower-packed (row-major) sum of the slabs: a row block of B
+// (rows [r0, r1) are elements [r0(r0+1)/2, r1(r1+1)/2)) can be packed as soon as its tiles exist
 __global__ __launch_bounds__(256) void sym_pack_kernel(const double* __restrict__ slab,
-                                                       int64_t stride, int nslab, int m, int M,
+                                                       int64_t stride, int nslab, int64_t e0,
+                                                       int64_t e1, int M,
                                                        double* __restrict__ packed) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t len = (int64_t)m * (m + 1) / 2;
-  if (e >= len) return;
+  const int64_t e = e0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= e1) return;
   int i = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
   while ((int64_t)(i + 1) * (i + 2) / 2 <= e) ++i;
   while ((int64_t)i * (i + 1) / 2 > e) --i;
@@ -178,11 +180,12 @@ __global__ __launch_bounds__(256) void sym_unpack_kernel(const double* __restric
   dst[e] = v;
 }
 
-hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, int m, int M,
-                           double* packed, hipStream_t s) {
-  const int64_t len = (int64_t)m * (m + 1) / 2;
-  hipLaunchKernelGGL(sym_pack_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, slab,
-                     slice_stride, nslab, m, M, packed);
+hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, int r0, int r1,
+                           int M, double* packed, hipStream_t s) {
+  const int64_t e0 = (int64_t)r0 * (r0 + 1) / 2, e1 = (int64_t)r1 * (r1 + 1) / 2;
+  if (r1 <= r0) return hipSuccess;
+  hipLaunchKernelGGL(sym_pack_kernel, dim3((unsigned)((e1 - e0 + 255) / 256)), dim3(256), 0, s,
+                     slab, slice_stride, nslab, e0, e1, M, packed);
   return hipGetLastError();
 }
 

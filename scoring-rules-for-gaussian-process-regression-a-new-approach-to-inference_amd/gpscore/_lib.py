@@ -22,6 +22,8 @@ GPS_OPT_GRAPH = 10
 GPS_OPT_PRED_PRE = 11
 GPS_OPT_DAG = 12
 GPS_OPT_DAG_TILES = 13
+GPS_OPT_FORK_MAX = 14
+GPS_OPT_AR_CHUNKS = 15
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")
 GPS_SURF_LOGS_ADD_NOISE = 1
@@ -191,6 +193,11 @@ class Context:
         """Replay the recursive factorisation from a captured hipGraph (default) or launch
         it eagerly."""
         self.call("gps_ctx_set_option", GPS_OPT_GRAPH, 1 if on else 0)
+
+    def set_ar_chunks(self, chunks):
+        """Sharded FITC: B's all-reduce in this many row blocks overlapped with the SYRK
+        (GPS_OPT_AR_CHUNKS, default 4; 1 = one all-reduce after the SYRK)."""
+        self.call("gps_ctx_set_option", GPS_OPT_AR_CHUNKS, int(chunks))
 
     def set_dag(self, on=True, tiles=None):
         """The persistent factorisation of the bottom diagonal blocks (GPS_OPT_DAG, default on)

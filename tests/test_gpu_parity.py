@@ -657,10 +657,14 @@ def test_persistent_factorisation_matches_recursion(gpu_ctx, n, tiles):
     y, yt = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n), np.sin(Xt.sum(1))
     th = (0.2, np.log(1.7) * np.ones(d), np.log(0.02))
     gp = gpscore.GP(ctx=gpu_ctx)
+    th_other = (0.5, np.log(0.9) * np.ones(d), np.log(0.05))
     runs = []
     try:
         for dag in (False, True, True):
             gpu_ctx.set_dag(dag, tiles)
+            # another θ first: the buffers then hold other values, so a replayed sequence that
+            # wrote nothing (or wrote elsewhere) cannot pass for the right one
+            gp.fit(X, y, th_other)
             r = gp.fit(X, y, th)
             mu, var = gp.predict(Xt, yt)
             runs.append((r, mu, var))

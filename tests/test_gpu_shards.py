@@ -42,7 +42,7 @@ def _run(gp, th, with_grad):
     return out
 
 
-def _sharded(P, X, y, Xt, yt, Z, th, with_grad):
+def _sharded(P, X, y, Xt, yt, Z, th, with_grad, ar_chunks=None):
     import gpscore
     from gpscore.dist import shard_rows
     _GROUP[0] += 1
@@ -54,6 +54,8 @@ def _sharded(P, X, y, Xt, yt, Z, th, with_grad):
         ctx = gpscore.Context(0)
         try:
             ctx.call("gps_comm_init_local", P, r, key)
+            if ar_chunks is not None:
+                ctx.set_ar_chunks(ar_chunks)
             gp = gpscore.GP(ctx=ctx)
             a, b = shard_rows(n, P, r)
             ta, tb = shard_rows(nt, P, r)
@@ -214,3 +216,19 @@ def test_local_group_reinit_and_duplicate_rank(gpu_ctx):
     finally:
         for c in (c0, c1, c2):
             c.close()
+
+
+def test_fitc_shards_chunked_allreduce_bitwise(gpu_ctx):
+    """GPS_OPT_AR_CHUNKS: B's exchange in row blocks, each all-reduced on the comm stream while
+    the next block's SYRK runs, gives the same bits as one all-reduce after the whole
+    SYRK — the slab values do not depend on the row blocks, and the packed sum is the same sum
+    in the same order — for the forward objectives, the LOO and predictive vectors and scores."""
+    X, y, Xt, yt, Z, th = _case(5000, 700, 700, 6, 47)  # m_pad = 768: 6 tile rows
+    runs = {c: _sharded(2, X, y, Xt, yt, Z, th, False, ar_chunks=c) for c in (1, 4, 6)}
+    base = runs[1]
+    for c in (4, 6):
+        for pa, pb in zip(runs[c], base):
+            assert pa["obj"] == pb["obj"], c
+            assert pa["sc"] == pb["sc"], c
+            for k in ("mu_loo", "var_loo", "mu", "var"):
+                assert np.array_equal(pa[k], pb[k]), (c, k)

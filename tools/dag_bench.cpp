@@ -47,6 +47,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ld, n * 8)); CK(hipMalloc(&info, 8));
   const int64_t ncnt = dag_cnt_ints(T);
   CK(hipMalloc(&cnt, ncnt * 4));
+  CK(hipMemset(cnt, 0, ncnt * 4));
   CK(hipMalloc(&tasks, nt * 4));
   CK(hipMalloc(&trace, (size_t)nt * 32));
   CK(hipMemcpy(A0, h.data(), bytes, hipMemcpyHostToDevice));
@@ -60,8 +61,7 @@ int main(int argc, char** argv) {
   auto launch = [&](bool tr, float* ms) {
     CK(hipMemcpy(A, A0, bytes, hipMemcpyDeviceToDevice));
     CK(hipMemset(Li, 0, bytes));
-    CK(hipMemset(cnt, 0, ncnt * 4));
-    CK(hipMemset(info, 0x7f, 8));
+    CK(hipMemset(info, 0x7f, 8));  // (the counters stay zero between launches: self-reset)
     CK(hipDeviceSynchronize());
     p.trace = tr ? trace : nullptr;
     CK(hipEventRecord(e0, 0));
