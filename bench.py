@@ -399,6 +399,12 @@ def fitc_cpu_baseline():
                              "unit — not the reference algorithm"}
 
 
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout): a long run keeps writing, so a
+    watchdog that reads silence as a hang sees the legs go by."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -436,8 +442,10 @@ def main():
         gp.fit(theta=th, return_loo=False)
         return gp.predict(with_scores=True)
 
+    log(f"{args.config}: warmup")
     for _ in range(args.warmup):
         unit()
+    log(f"{args.config}: timed pass")
     # headline pass: production configuration (side-stream overlap on, no events)
     t_full = timed(ctl, ctx, unit, args.steps)
     ms_full = 1e3 * t_full / args.steps
@@ -478,6 +486,7 @@ def main():
                               "note": "second timed pass, overlap off, hipEvents around each launch"},
     }
 
+    log("headline done: %.2f ms/step" % ms_full)
     # ---------------- gradients (next-1: one GD iteration = fwd + analytic bwd) -------------
     if not args.no_grad:
         grad = {}
@@ -494,6 +503,7 @@ def main():
                        "(fit + A^-1 + [A^-1 diag(c) A^-1] + dA/dtheta contraction); flop = n^3 "
                        "(NLML) / 2n^3 (LOO) at n_pad", **grad}
 
+    log("gradient leg done")
     # ---------------- next-2: block-LOO objectives, one GD iteration each (C2) ----------------
     if not args.no_block:
         from gpscore.gp import es_draws
@@ -516,6 +526,7 @@ def main():
                             "note": "value + analytic gradient per GD iteration (KF:487-543, "
                                     "K20:655-720, KF:607-663)", **blk}
 
+    log("block-LOO leg done")
     # ---------------- FITC (rows sharded, RCCL all-reduce) ----------------
     if not args.no_fitc:
         from gpscore.dist import shard_rows
@@ -555,6 +566,7 @@ def main():
                 fgp.fit(theta=thf, return_loo=False)
                 return fgp.predict(with_scores=True)
 
+            log(f"FITC {leg}: warmup")
             for _ in range(args.warmup):
                 funit()
             tf = timed(ctl, ctx, funit, args.steps)
@@ -591,8 +603,10 @@ def main():
             ctx.call("gps_comm_destroy")
         res["fitc"] = fitc
 
+    log("FITC legs done")
     res["surface"] = surface_leg(ctx, args.steps, rank == 0 and world == 1 and not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu:
+        log("CPU baseline (about two minutes)")
         cb, ref = cpu_baseline(args.config)
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
@@ -600,8 +614,10 @@ def main():
                                f"{args.config} inputs",
                          "metric": "normwise relative error (vectors: max|a-b|/max|b|; scalars: "
                                    "|a-b|/max(1,|b|))", **parity(got, ref)}
+        log("C1 leg")
         res["c1"] = c1_leg(ctx, args.steps)
         if "fitc" in res and "C4" in res["fitc"]:
+            log("FITC C4 CPU baseline")
             res["fitc"]["C4"]["cpu_baseline"] = fitc_cpu_baseline()
     if args.rehearse:
         res["rehearsal"] = "all ranks on device 0, no RCCL: not a measurement"

@@ -101,6 +101,8 @@ enum {
                              as workgroup slots free up; 0 (default): equal priority */
   GPS_OPT_DAG_TILES = 13, /* largest block (in 128-tiles, 2..64, default 20) the persistent
                             factorisation takes */
+  GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
+                             flight per load group (2, 3 (default) or 4).  Same values bitwise. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -103,6 +103,7 @@ struct gps_ctx {
   bool pred_pre = true;                // GPS_OPT_PRED_PRE
   bool dag = true;                     // GPS_OPT_DAG: persistent factorisation of the bottom blocks
   int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
+  int dag_group = 3;                   // GPS_OPT_DAG_GROUP
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   int64_t dag_cnt_used = 0;
@@ -429,6 +430,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     d.tasks = static_cast<const uint32_t*>(it->second.first.p); d.ntasks = it->second.second;
     d.cnt = static_cast<int*>(ctx->dag_cnt.p) + ctx->dag_cnt_used;
     d.spin_ticks = 200000000ull;  // 2 s at the 100 MHz real-time clock
+    d.group = ctx->dag_group;
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
@@ -581,7 +583,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
-      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_cnt.p};
+      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_cnt.p};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
@@ -1221,6 +1223,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
     case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;
     case GPS_OPT_DAG: ctx->dag = value != 0; return 0;
+    case GPS_OPT_DAG_GROUP:
+      ARGCHK(value >= 2 && value <= 4, "GPS_OPT_DAG_GROUP must be 2, 3 or 4");
+      ctx->dag_group = value;
+      return 0;
     case GPS_OPT_DAG_TILES:
       ARGCHK(value >= 2 && value <= 64, "GPS_OPT_DAG_TILES must be in 2..64");
       ctx->dag_tiles = value;

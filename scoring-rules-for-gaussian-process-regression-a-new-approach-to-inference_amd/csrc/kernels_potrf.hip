@@ -487,17 +487,19 @@ __device__ __forceinline__ void wave_gemm32(const double* Ap, int64_t lda, const
             acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][i][kk], b[u][j][kk], acc[i][j], 0, 0, 0);
     }
   };
-  Frag fa0, fb0, fa1, fb1;
-  int c = 0;
-  if (c < nc) load_group(c, fa0, fb0);
-  while (c < nc) {
-    if (c + G < nc) load_group(c + G, fa1, fb1);
-    mma_group(c, fa0, fb0);
-    c += G;
-    if (c >= nc) break;
-    if (c + G < nc) load_group(c + G, fa0, fb0);
-    mma_group(c, fa1, fb1);
-    c += G;
+  {
+    Frag fa0, fb0, fa1, fb1;
+    int c = 0;
+    if (c < nc) load_group(c, fa0, fb0);
+    while (c < nc) {
+      if (c + G < nc) load_group(c + G, fa1, fb1);
+      mma_group(c, fa0, fb0);
+      c += G;
+      if (c >= nc) break;
+      if (c + G < nc) load_group(c + G, fa0, fb0);
+      mma_group(c, fa1, fb1);
+      c += G;
+    }
   }
 }
 

@@ -682,6 +682,31 @@ def test_persistent_factorisation_matches_recursion(gpu_ctx, n, tiles):
     assert abs(r1.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
+@pytest.mark.parametrize("n", [2560, 5000])
+def test_persistent_factorisation_load_groups_bitwise(gpu_ctx, n):
+    """GPS_OPT_DAG_GROUP only changes how many operand chunks a strip task has in flight, not the
+    MFMA order: every group depth gives the same bits."""
+    import gpscore
+    from gpscore import _lib
+    rng = np.random.default_rng(n)
+    d = 5
+    X = rng.standard_normal((n, d))
+    y = np.cos(X.sum(1)) + 0.1 * rng.standard_normal(n)
+    th = (0.1, np.log(1.5) * np.ones(d), np.log(0.03))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    runs = []
+    try:
+        for g in (3, 4, 2):
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_GROUP, g)
+            r = gp.fit(X, y, th)
+            runs.append(r)
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_GROUP, 3)
+    for r in runs[1:]:
+        assert r.objectives == runs[0].objectives
+        assert np.array_equal(r.mu_loo, runs[0].mu_loo) and np.array_equal(r.var_loo, runs[0].var_loo)
+
+
 def test_persistent_factorisation_potrf_exports(gpu_ctx):
     """gps_potrf (L out of the persistent kernel's TRSM tasks and leaves) and the non-PD minor
     reported from inside a persistent block."""
