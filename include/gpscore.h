@@ -218,7 +218,10 @@ int gps_full_blockloo_es(gps_ctx* ctx, int kind, const double* theta, int n_ell,
                          double* grad, double* fold_values);
 /* FITC, DSS or KC; grad (2 + n_ell) and grad_z (m×d, row-major) may be NULL: the
  * `.backward()` at K20:587 / K20:720 w.r.t. theta and the inducing inputs, which the scripts
- * move too (K20:593, 726).  All rows on one rank (no communicator). */
+ * move too (K20:593, 726).  With a communicator the rows may be sharded: the nfold folds are
+ * those of the GLOBAL rows ([⌊fN/k⌋, ⌊(f+1)N/k⌋), KF:496-499) and each must lie inside one
+ * rank's rows (gpscore.dist.fold_shard_rows), else every rank returns -1; every rank gets the
+ * global value, gradients and all nfold fold_values. */
 int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, int objective,
                       double* value, double* grad, double* grad_z, double* fold_values);
 /* ES(m, c, shape1, data_y, num_sim, beta) (KF:70-101) of one Gaussian N(m, C) (b×b,

@@ -150,6 +150,7 @@ struct gps_ctx {
   // FITC gradient: the fold's G_f, E_f, G_fE_f and F = Gblk E; energy score: work area, draws
   DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
   DBuf ebuf_aux[3], bPIs, bRW;  // concurrent ES folds: work areas of the aux streams, C_f, r_f / w_f
+  DBuf bfv;                       // sharded FITC block-LOO: row counts, then the fold values
   size_t bL_zeroed = 0;
   size_t lm_zeroed = 0, lb_zeroed = 0;
   int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
@@ -764,10 +765,9 @@ std::vector<int64_t> fold_bounds(int64_t n, int nfold) {
 }
 
 // padded edge of the largest fold
-int64_t fold_pad(int64_t n, int nfold) {
-  const std::vector<int64_t> bnd = fold_bounds(n, nfold);
+int64_t bounds_pad(const std::vector<int64_t>& bnd) {
   int64_t bmax = 1;
-  for (int f = 0; f < nfold; ++f) bmax = std::max(bmax, bnd[f + 1] - bnd[f]);
+  for (size_t f = 0; f + 1 < bnd.size(); ++f) bmax = std::max(bmax, bnd[f + 1] - bnd[f]);
   return pad_to(bmax);
 }
 
@@ -968,12 +968,12 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
 }
 
 template <class GetP, class GDst, class GDone>
-int blockloo_folds(gps_ctx* ctx, int64_t n, int nfold, int objective, const double* alpha,
+int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective, const double* alpha,
                    const double* y, GetP getP, bool want_grad, GDst gdst, GDone gdone, double* g,
                    const EsArgs* es, double* vals) {
   hipStream_t s = ctx->stream;
-  const std::vector<int64_t> bnd = fold_bounds(n, nfold);
-  const int64_t bp = fold_pad(n, nfold);
+  const int nfold = (int)bnd.size() - 1;
+  const int64_t bp = bounds_pad(bnd);
   HIPCHK(ensure(ctx->bP, (size_t)bp * bp * 8));
   if (ctx->bL.cap < (size_t)bp * bp * 8 || ctx->bL_zeroed != (size_t)bp) {
     HIPCHK(ensure(ctx->bL, (size_t)bp * bp * 8));
@@ -1119,7 +1119,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
                  &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->dag_cnt};
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->bfv, &ctx->dag_cnt};
 }
 
 extern "C" {
@@ -2271,7 +2271,7 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
   auto gdst = [&](int64_t a, int64_t) { return std::make_pair(Gblk + a * np + a, np); };
   auto gdone = [](int, int64_t, int64_t) { return 0; };
   std::vector<double> fv(nfold);
-  if ((rc = blockloo_folds(ctx, n, nfold, objective, ctx->alpha.d(), ctx->y.d(), getP,
+  if ((rc = blockloo_folds(ctx, fold_bounds(n, nfold), objective, ctx->alpha.d(), ctx->y.d(), getP,
                            grad != nullptr, gdst, gdone, grad ? ctx->gu.d() : nullptr, es,
                            fv.data())))
     return rc;
@@ -2428,6 +2428,54 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
   return 0;
 }
 
+// The folds of the GLOBAL rows (KF:496-499: [⌊fN/k⌋, ⌊(f+1)N/k⌋)) that lie in this rank's rows,
+// as local bounds, and their global indices.  Sharded: the ranks' row counts are all-reduced
+// (every rank then sees the same shard layout, so all agree on a refusal); a fold that
+// straddles two shards is refused (gpscore.dist.fold_shard_rows shards on fold boundaries).
+static int local_folds(gps_ctx* ctx, int nfold, std::vector<int64_t>& bnd, std::vector<int>& fid) {
+  const int64_t n = ctx->fn;
+  bnd.clear();
+  fid.clear();
+  if (!sharded(ctx)) {
+    ARGCHK(n >= nfold, "fewer rows than folds");
+    bnd = fold_bounds(n, nfold);
+    for (int f = 0; f < nfold; ++f) fid.push_back(f);
+    return 0;
+  }
+  const int P = ctx->nranks;
+  hipStream_t s = ctx->stream;
+  HIPCHK(ensure(ctx->bfv, (size_t)std::max(P, 64) * 8));
+  std::vector<double> cnt((size_t)P, 0.0);
+  cnt[ctx->rank] = (double)n;
+  HIPCHK(hipMemcpyAsync(ctx->bfv.p, cnt.data(), (size_t)P * 8, hipMemcpyHostToDevice, s));
+  if (int rc = allreduce_sum(ctx, ctx->bfv.d(), (size_t)P, s)) return rc;
+  HIPCHK(hipMemcpyAsync(cnt.data(), ctx->bfv.p, (size_t)P * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  int64_t N = 0, off = 0;
+  for (int r = 0; r < P; ++r) {
+    if (r < ctx->rank) off += (int64_t)cnt[r];
+    N += (int64_t)cnt[r];
+  }
+  ARGCHK(N >= nfold, "fewer rows than folds");
+  const std::vector<int64_t> gb = fold_bounds(N, nfold);
+  int64_t e = 0;
+  for (int r = 0; r + 1 < P; ++r) {  // every interior shard boundary must be a fold boundary
+    e += (int64_t)cnt[r];
+    for (int f = 0; f < nfold; ++f)
+      ARGCHK(!(gb[f] < e && e < gb[f + 1]),
+             "sharded FITC block-LOO: a fold straddles two shards (shard the rows on fold "
+             "boundaries: gpscore.dist.fold_shard_rows)");
+  }
+  for (int f = 0; f < nfold; ++f)
+    if (gb[f] >= off && gb[f + 1] <= off + n && gb[f + 1] > gb[f]) {
+      if (bnd.empty()) bnd.push_back(gb[f] - off);
+      bnd.push_back(gb[f + 1] - off);
+      fid.push_back(f);
+    }
+  ARGCHK(!fid.empty(), "sharded FITC block-LOO: this rank holds no whole fold");
+  return 0;
+}
+
 // FITC block-LOO objective (K20:523-587 DSS, K20:655-720 KC): P_f = ((Q+Λ)⁻¹)_ff =
 // Λ_f⁻¹ − U_fU_fᵀ with U = Λ⁻¹K Lb⁻ᵀ (one n×m TRMM), α = (y − Kc)/λ.  With grad / grad_z the
 // `.backward()` at K20:587 / 720 w.r.t. θ and the inducing inputs (moved at K20:593 / 726):
@@ -2436,7 +2484,9 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
 //   G_K  = −2Λ⁻¹F + 2Λ⁻¹K(B⁻¹T) − 2diag(M_ii)KKm⁻¹ − vcᵀ − αŵᵀ,  ŵ = Km⁻¹Kᵀv,
 //   G_Km = S + Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹ + ½(ŵcᵀ + cŵᵀ),
 //   M_ii = −(G_ii − 2F_i·K_i + (KS)_i·K_i)/λ_i² − v_iα_i   (blk_mdiag, kernels_block.hip),
-// contracted with ∂K/∂θ, ∂K/∂Z like gps_fitc_grad.  All rows on one rank.
+// contracted with ∂K/∂θ, ∂K/∂Z like gps_fitc_grad.  Row-sharded like gps_fitc_grad when every
+// fold lies in one rank's rows (local_folds): the folds are local, the fold values and the
+// n-sums Kᵀ(g/λ), [S | T], Kᵀv, [Kᵀdiag(M_ii)K | ΣM_ii] and the contraction are all-reduced.
 int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, int objective,
                       double* value, double* grad, double* grad_z, double* fold_values) {
   if (int rc = bind(ctx)) return rc;
@@ -2444,7 +2494,6 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   ARGCHK(objective == GPS_BLOCK_DSS || objective == GPS_BLOCK_KC,
          "objective must be GPS_BLOCK_DSS or GPS_BLOCK_KC");
   ARGCHK(value != nullptr, "value is NULL");
-  ARGCHK(!sharded(ctx), "FITC block-LOO needs every row on one rank");
   double o[GPS_N_OBJ];
   int rc;
   if ((rc = fitc_fit_core(ctx, theta, n_ell, o))) return rc;
@@ -2452,11 +2501,14 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   const Theta& th = ctx->fth;
   const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
   const int d = ctx->fd;
-  ARGCHK(n >= nfold, "fewer rows than folds");
+  const bool shard = sharded(ctx);
+  std::vector<int64_t> bnd;
+  std::vector<int> fid;
+  if ((rc = local_folds(ctx, nfold, bnd, fid))) return rc;
   hipStream_t s = ctx->stream;
   const bool want = grad != nullptr || grad_z != nullptr;
   const int64_t ldr = want ? 3 * mp : mp;  // [U | E | K Km⁻¹]; U's slot later holds KS, KB⁻¹T
-  const int64_t bp = fold_pad(n, nfold);
+  const int64_t bp = bounds_pad(bnd);
   HIPCHK(ensure(ctx->fR, (size_t)np * ldr * 8));
   HIPCHK(ensure(ctx->fgv, (size_t)13 * np * 8));
   double* U = ctx->fR.d();
@@ -2485,7 +2537,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   double *Binv = nullptr, *Kminv = nullptr, *Sm = nullptr, *Tm = nullptr, *BT = nullptr,
          *KmD = nullptr, *F = nullptr;
   if (want) {
-    HIPCHK(ensure(ctx->fgB, (size_t)6 * mp * mp * 8));
+    HIPCHK(ensure(ctx->fgB, (size_t)(shard ? 7 : 6) * mp * mp * 8));
     double* Bb = ctx->fgB.d();
     Binv = Bb; Kminv = Bb + mp * mp; Sm = Bb + 2 * mp * mp; Tm = Bb + 3 * mp * mp;
     BT = Bb + 4 * mp * mp; KmD = Bb + 5 * mp * mp;
@@ -2533,10 +2585,17 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     HIPCHK(launch_pad_copy(ctx->bG.d(), bp + 1, gd + a, 1, (int)b, 1, (int)b, 1, 0, s));
     return 0;
   };
-  std::vector<double> fv(nfold);
-  if ((rc = blockloo_folds(ctx, n, nfold, objective, alpha, ctx->fy.d(), getP, want, gdst, gdone,
-                           want ? gg : nullptr, nullptr, fv.data())))
+  std::vector<double> fvl(fid.size()), fv((size_t)nfold, 0.0);
+  if ((rc = blockloo_folds(ctx, bnd, objective, alpha, ctx->fy.d(), getP, want, gdst, gdone,
+                           want ? gg : nullptr, nullptr, fvl.data())))
     return rc;
+  for (size_t j = 0; j < fid.size(); ++j) fv[fid[j]] = fvl[j];
+  if (shard) {  // every fold's value on every rank (each fold is computed by exactly one rank)
+    HIPCHK(hipMemcpyAsync(ctx->bfv.p, fv.data(), (size_t)nfold * 8, hipMemcpyHostToDevice, s));
+    if ((rc = allreduce_sum(ctx, ctx->bfv.d(), (size_t)nfold, s))) return rc;
+    HIPCHK(hipMemcpyAsync(fv.data(), ctx->bfv.p, (size_t)nfold * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
   double tot = 0.0;
   for (int f = 0; f < nfold; ++f) tot += fv[f];
   *value = tot;
@@ -2550,10 +2609,11 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   HIPCHK(launch_vec_mul(gg, ctx->ilam.d(), (int)np, ulam, s));
   HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr,
                        ctx->fslab.d(), s));
+  if ((rc = allreduce_sum(ctx, tku, (size_t)mp, s))) return rc;
   HIPCHK(launch_gemv_full(Binv, mp, tku, tbt, (int)mp, (int)mp, s));
   HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, tbt, zv, (int)np, (int)mp, s));
   HIPCHK(launch_fitc_grad_v(ulam, zv, ctx->lam.d(), (int)n, v, s));
-  {  // T = KᵀΛ⁻¹F, S = EᵀF (m×m, n·m² each)
+  {  // T = KᵀΛ⁻¹F, S = EᵀF (m×m, n·m² each; [S | T] contiguous: one all-reduce)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = F; p.ldb = mp; p.C = Tm; p.ldc = mp;
     p.kscale = ctx->ilam.d(); p.M = (int)mp; p.N = (int)mp; p.K = (int)np;
@@ -2563,6 +2623,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     q.M = (int)mp; q.N = (int)mp; q.K = (int)np;
     if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, q))) return rc;
   }
+  if ((rc = allreduce_sum(ctx, Sm, (size_t)2 * mp * mp, s))) return rc;
   if ((rc = gemm_nn(Binv, mp, Tm, BT, mp, mp))) return rc;          // B⁻¹T
   if ((rc = gemm_nn(ctx->Knm.d(), mp, Sm, U, ldr, np))) return rc;  // K S (into U's slot)
   {
@@ -2573,17 +2634,29 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   if ((rc = gemm_nn(ctx->Knm.d(), mp, BT, U, ldr, np))) return rc;      // K B⁻¹T
   if ((rc = gemm_nn(ctx->Knm.d(), mp, Kminv, RC, ldr, np))) return rc;  // K Km⁻¹
   // ŵ = Km⁻¹Kᵀv;  Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹;  Σ M_ii
+  // [P | Σ M_ii | (pad) | Kᵀv]: P = Kᵀdiag(M_ii)K lower-packed (m(m+1)/2) when sharded, else
+  // the padded lower tiles (gps_fitc_grad's layout)
   HIPCHK(ensure(ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
+  const int64_t plen = shard ? m * (m + 1) / 2 : mp * mp;
+  const int64_t off_tw = (plen + 2) / 2 * 2;
   double* red = ctx->fgred.d();
-  double* tw = red + mp * mp;
-  double* smd = red + mp * mp + mp;
+  double* smd = red + plen;
+  double* tw = red + off_tw;
   HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, v, nullptr, tw, nullptr,
                        ctx->fslab.d(), s));
+  if ((rc = allreduce_sum(ctx, tw, (size_t)mp, s))) return rc;
   HIPCHK(launch_gemv_full(Kminv, mp, tw, what, (int)mp, (int)mp, s));
-  if ((rc = fitc_syrk(ctx, md, nullptr, red))) return rc;
+  if ((rc = fitc_syrk(ctx, md, nullptr, red, shard))) return rc;
   HIPCHK(launch_dot(md, nullptr, (int)np, smd, s));
-  HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
-  if ((rc = gemm_nn(red, mp, Kminv, Tm, mp, mp))) return rc;
+  if ((rc = allreduce_sum(ctx, red, (size_t)(plen + 1), s))) return rc;
+  double* Pfull = red;
+  if (shard) {
+    Pfull = ctx->fgB.d() + 6 * mp * mp;
+    HIPCHK(launch_sym_unpack(red, (int)m, (int)mp, nullptr, 1, Pfull, s));
+  } else {
+    HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
+  }
+  if ((rc = gemm_nn(Pfull, mp, Kminv, Tm, mp, mp))) return rc;
   if ((rc = gemm_nn(Kminv, mp, Tm, KmD, mp, mp))) return rc;
   // contractions with ∂Knm/∂θ, ∂Knm/∂Z and ∂Kmm/∂θ, ∂Kmm/∂Z
   const int passes = fitc_contract_passes(d);
@@ -2611,7 +2684,8 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * 3 * np * mp);
     HIPCHK(launch_fitc_grad_contract(p, out1, out1 + passes * 17, s));
   }
-  {
+  if ((rc = allreduce_sum(ctx, out1, (size_t)outlen, s))) return rc;
+  {  // the m×m contraction: every operand is global by now (replicated on every rank)
     FitcContractParams p = cp;
     p.xr = ctx->Z.d(); p.xc = ctx->Z.d(); p.nr = (int)m; p.nc = (int)m; p.nc_pad = (int)mp;
     p.R[0] = Sm; p.ldr[0] = mp; p.coef[0] = 1.0;

@@ -30,6 +30,18 @@ def shard_rows(n, nranks, rank):
     return start, start + q + (1 if rank < r else 0)
 
 
+def fold_shard_rows(n, nfold, nranks, rank):
+    """Rows of `rank` when n rows in nfold block-LOO folds ([int(f·n/k), int((f+1)·n/k)),
+    KF:496-499) are sharded over nranks on fold boundaries: the folds are split as evenly as
+    shard_rows splits rows, so every fold lies inside one rank's rows — what the sharded
+    FITC block-LOO (gps_fitc_blockloo) needs.  Returns (start, stop)."""
+    if not 1 <= nranks <= nfold:
+        raise ValueError("need 1 <= nranks <= nfold (every rank holds at least one fold)")
+    f0, f1 = shard_rows(nfold, nranks, rank)
+    bound = (lambda f: int(n) if f == nfold else int(f * int(n) / nfold))
+    return bound(f0), bound(f1)
+
+
 def global_target_stats(y_local, group=None):
     """(mean, unbiased var, n_total) of the training targets over all ranks —
     what trivial_loss / SMSE need (KF:112-114, 130).  Two passes over float64 host

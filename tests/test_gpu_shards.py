@@ -160,19 +160,70 @@ def test_fitc_shards_empty_test_shard(gpu_ctx):
              "fitc_shards_empty_test")
 
 
-def test_block_loo_refuses_shards(gpu_ctx):
-    """FITC block-LOO needs all rows on one rank; a sharded context reports it (no hang)."""
+def _blockloo_sharded(P, X, y, Z, th, nfold, objective, rows):
     import gpscore
-    X, y, Xt, yt, Z, th = _case(400, 10, 30, 3, 44)
-    ctx = gpscore.Context(0)
-    try:
-        ctx.call("gps_comm_init_local", 1, 0, 999999)
-        gp = gpscore.GP(ctx=ctx)
-        gp.set_data(X, y, kind="fitc", Z=Z)
-        with pytest.raises(gpscore.GpsError):
-            gp.block_loo(th, "kc")
-    finally:
-        ctx.close()
+    _GROUP[0] += 1
+    key = _GROUP[0]
+    n = len(y)
+    stats = (float(y.mean()), float(y.var(ddof=1)))
+
+    def rank_job(r):
+        ctx = gpscore.Context(0)
+        try:
+            ctx.call("gps_comm_init_local", P, r, key)
+            gp = gpscore.GP(ctx=ctx)
+            a, b = rows(n, nfold, P, r)
+            gp.set_data(X[a:b], y[a:b], kind="fitc", Z=Z, n_total=n, ytr_stats=stats)
+            try:
+                return gp.block_loo(th, objective, nfold=nfold, grad=True)
+            except gpscore.GpsError as e:
+                return e
+            finally:
+                ctx.call("gps_comm_destroy")
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(max_workers=P) as ex:
+        return list(ex.map(rank_job, range(P)))
+
+
+@pytest.mark.parametrize("P,nfold,objective", [(2, 4, "kc"), (3, 6, "dss"), (4, 4, "kc")])
+def test_fitc_blockloo_shards(gpu_ctx, P, nfold, objective):
+    """FITC block-LOO (K20:523-587 DSS, K20:655-720 KC) with the rows sharded on fold
+    boundaries (dist.fold_shard_rows): every rank returns the unsharded value, all fold values,
+    and the θ- and Z-gradients (a shard split only reorders the n-sums)."""
+    import gpscore
+    from gpscore.dist import fold_shard_rows
+    X, y, _, _, Z, th = _case(4000, 10, 40, 4, 45 + P)
+    gp = gpscore.GP(ctx=gpu_ctx)
+    gp.set_data(X, y, kind="fitc", Z=Z)
+    v0, g0, f0, gz0 = gp.block_loo(th, objective, nfold=nfold, grad=True)
+    parts = _blockloo_sharded(P, X, y, Z, th, nfold, objective,
+                              lambda n, k, p, r: fold_shard_rows(n, k, p, r))
+    errs = {}
+    for res in parts:
+        assert not isinstance(res, Exception), res
+        v, g, f, gz = res
+        errs["value"] = max(errs.get("value", 0.0), abs(v - v0) / abs(v0))
+        errs["folds"] = max(errs.get("folds", 0.0), nrel(f, f0))
+        errs["grad"] = max(errs.get("grad", 0.0), nrel(g, g0))
+        errs["grad_Z"] = max(errs.get("grad_Z", 0.0), nrel(gz, gz0))
+    caps = {"value": 1e-10, "folds": 1e-10, "grad": 1e-8, "grad_Z": 1e-8}
+    record_floors(f"fitc_blockloo_shards_P{P}_{objective}", errs, {}, caps)
+    print(errs)
+    assert all(errs[k] <= caps[k] for k in caps), errs
+
+
+def test_fitc_blockloo_refuses_straddling_folds(gpu_ctx):
+    """Shards that cut a fold (contiguous row shards of 4001 rows over 2 ranks, 4 folds): every
+    rank reports the error — none is left waiting in an all-reduce."""
+    import gpscore
+    from gpscore.dist import shard_rows
+    X, y, _, _, Z, th = _case(4001, 10, 30, 3, 44)
+    parts = _blockloo_sharded(2, X, y, Z, th, 4, "kc",
+                              lambda n, k, p, r: shard_rows(n, p, r))
+    assert all(isinstance(r, gpscore.GpsError) for r in parts), parts
+    assert all("straddles" in str(r) for r in parts), parts
 
 
 def test_local_group_reinit_and_duplicate_rank(gpu_ctx):

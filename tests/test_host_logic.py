@@ -35,6 +35,23 @@ def test_shard_rows_partition(n, p):
     assert spans == O.shard_bounds(n, p)
 
 
+@pytest.mark.parametrize("n,k,p", [(4001, 4, 2), (40000, 4, 4), (6001, 6, 3), (1003, 64, 8),
+                                   (10, 4, 1)])
+def test_fold_shard_rows_nest_folds(n, k, p):
+    """Shards on fold boundaries (the sharded FITC block-LOO): a partition of the rows in which
+    every fold [int(f·n/k), int((f+1)·n/k)) (KF:496-499) lies inside one shard."""
+    from gpscore.dist import fold_shard_rows
+    spans = [fold_shard_rows(n, k, p, r) for r in range(p)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c and b > a
+    bounds = [n if f == k else int(f * n / k) for f in range(k + 1)]
+    for a, b in spans:
+        assert a in bounds and b in bounds
+    with pytest.raises(ValueError):
+        fold_shard_rows(n, k, k + 1, 0)
+
+
 def test_errors_are_runtime_errors():
     from gpscore import GpsError, NotPositiveDefinite
     assert issubclass(NotPositiveDefinite, RuntimeError)  # caught as in KF:726, K20:784
