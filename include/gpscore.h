@@ -101,6 +101,11 @@ enum {
                              as workgroup slots free up; 0 (default): equal priority */
   GPS_OPT_DAG_TILES = 13, /* largest block (in 128-tiles, 2..64, default 20) the persistent
                             factorisation takes */
+  GPS_OPT_STREAM_K = 18,  /* 1 (default): a 128-tile GEMM launch with uniform K ranges (the
+                             trailing-update SYRKs) whose last round of workgroup slots would be at
+                             most 3/4 full splits that round's tiles into equal K runs over every
+                             slot (in-launch fixed-order combine); 0: one workgroup per tile.
+                             Process-wide. */
   GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
                              flight per load group (2, 3 (default) or 4).  Same values bitwise. */
 };

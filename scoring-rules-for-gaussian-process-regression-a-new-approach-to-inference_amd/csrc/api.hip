@@ -106,6 +106,7 @@ struct gps_ctx {
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
+  DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
   int64_t dag_cnt_used = 0;
   struct PrePass {                     // work potrf_inv launches on aux[0] once the top-level
     int kind = 0;                      // L11⁻¹ is final: PRE_FITC_Q (the q column tiles [0, n1))
@@ -317,6 +318,10 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
     HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8));
     q.ws = ws.d();
     q.ws_cap = kSplitWsDoubles;
+    if (st == ctx->stream && ctx->sk_cnt.p) {  // the stream-K tail's tickets (main stream only)
+      q.sk_cnt = static_cast<int*>(ctx->sk_cnt.p);
+      q.sk_slots = 2 * ctx->ncu;
+    }
   }
   std::string tag = gemm_tag(al, bl, epi, p);
   if (ctx->prof > 1) {  // per-shape accounting (gps_prof_enable(ctx, 2))
@@ -578,7 +583,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
       (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->fork_max, (uintptr_t)ctx->gemm_map,
-      (uintptr_t)g_tiny_gemm, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
+      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
       (uintptr_t)ctx->ws_side.p, (uintptr_t)pre,
       // the pre-pass's operands (only when it is part of the sequence)
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
@@ -1119,7 +1124,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
                  &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->bfv, &ctx->dag_cnt};
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->bfv, &ctx->dag_cnt, &ctx->sk_cnt};
 }
 
 extern "C" {
@@ -1151,6 +1156,8 @@ int gps_ctx_create(int device, gps_ctx** out) {
   HIPCHK(hipHostMalloc((void**)&ctx->hinfo, 16, hipHostMallocDefault));
   HIPCHK(ensure(ctx->info, 16));
   HIPCHK(ensure(ctx->small, 256 * sizeof(double)));
+  HIPCHK(ensure(ctx->sk_cnt, (size_t)kStreamKTiles * sizeof(int)));
+  HIPCHK(hipMemset(ctx->sk_cnt.p, 0, (size_t)kStreamKTiles * sizeof(int)));
   *out = ctx;
   return 0;
 }
@@ -1219,6 +1226,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->ar_chunks = value;
       return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
+    case GPS_OPT_STREAM_K: g_stream_k = value != 0; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
     case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;

@@ -69,6 +69,11 @@ struct GemmParams {
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
+  int* sk_cnt;               // stream-K tail (launch_gemm): per-tile arrival tickets, zero at the
+                             // launch and left zero; partial tiles go to ws.  NULL: no stream-K
+  int sk_slots;              // workgroup slots of the chip (2 per CU for the 128-tile kernel)
+  // set by launch_gemm for the stream-K tail: tiles [sk_dp, tiles) are split over sk_wgs blocks
+  int sk_dp, sk_wgs;
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
@@ -76,6 +81,8 @@ struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
+extern int g_stream_k;   // 1: the stream-K tail of uniform-K 128-tile launches (launch_gemm)
+constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)
 
 // ------------------------------------------------------------ device reductions
 // fixed-order wave / block sums (no atomics anywhere: results are bitwise reproducible)

@@ -127,7 +127,10 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 
 template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
-                                          double* smem);
+                                          double* smem, int kb_o = -1, int ke_o = -1,
+                                          double* part = nullptr);
+template <int ALAY, int BLAY>
+__device__ void gemm_sk_block(const GemmParams& p, int s, double* smem);
 
 template <int ALAY, int BLAY, int EPI, int TILE>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
@@ -136,15 +139,125 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
   // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
-
+  if constexpr (EPI == EPI_STORE && TILE == 128) {
+    if (p.sk_wgs > 0 && (int)blockIdx.x >= p.sk_dp) {  // the stream-K tail (launch_gemm)
+      gemm_sk_block<ALAY, BLAY>(p, (int)blockIdx.x - p.sk_dp, smem);
+      return;
+    }
+  }
+  const int nblk = p.sk_wgs > 0 ? p.sk_dp : (int)gridDim.x;
   int ti, tj;
-  if (!tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj)) return;
+  if (!tile_of(p, remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x, ti, tj)) return;
   gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, blockIdx.y, smem);
+}
+
+// EPI_STORE epilogue: C = alpha·acc (+ beta·C) for this thread's accumulators
+template <int TILE>
+__device__ __forceinline__ void store_acc(const GemmParams& p, int ti, int tj, int kslice,
+                                          const d4 (&acc)[TILE / 32][TILE / 32]) {
+  constexpr int WT = TILE / 2, MI = WT / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lrow = lane >> 4, lcol = lane & 15;
+  const int row0 = ti * TILE, col0 = tj * TILE;
+  double* Cb = p.C + (int64_t)kslice * p.c_kslice_stride;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + wr * WT + mi * 16 + lrow + 4 * r;
+      double* crow = Cb + (int64_t)row * p.ldc + col0 + wc * WT + lcol;
+#pragma unroll
+      for (int ni = 0; ni < MI; ++ni) {
+        double v = p.alpha * acc[mi][ni][r];
+        if (p.beta != 0.0) v = fma(p.beta, crow[ni * 16], v);
+        crow[ni * 16] = v;
+      }
+    }
+}
+
+// Stream-K tail of a 128-tile EPI_STORE launch with uniform K ranges (launch_gemm decides): the
+// tiles [sk_dp, tiles) that would fill only part of a last round of workgroup slots are cut
+// into sk_wgs equal runs of 16-deep K slices, one per workgroup (block s runs iterations
+// [s·I/S, (s+1)·I/S) of the I = tiles·K/16 of the tail).  A run that covers part of a tile
+// writes its partial accumulators to workspace slot (tile + s) — distinct for every (tile,
+// block) pair, since runs are contiguous and ordered — publishes them (stores drained, agent
+// release, relaxed ticket) and the last arriver of the tile (agent acquire) sums the partials
+// in block order and runs the C epilogue: a fixed summation order, so the result is bitwise
+// reproducible (cdna_hip_programming.md §5 "In-launch split-K reduction", plain-store recipe).
+// The last arriver also zeroes the tile's ticket for the next launch.
+template <int ALAY, int BLAY>
+__device__ void gemm_sk_block(const GemmParams& p, int s, double* smem) {
+  constexpr int TILE = 128, MI = TILE / 32, TT = TILE * TILE;
+  const int tiles = p.lower_out ? p.tiles_m * (p.tiles_m + 1) / 2 : p.tiles_m * p.tiles_n;
+  const int nk = p.K / BK;
+  const int64_t I = (int64_t)(tiles - p.sk_dp) * nk, S = p.sk_wgs;
+  auto bnd = [&](int64_t q) { return q * I / S; };
+  auto owner = [&](int64_t x) {  // the block whose run holds iteration x
+    int64_t q = x * S / I;
+    while (q + 1 < S && bnd(q + 1) <= x) ++q;
+    while (q > 0 && bnd(q) > x) --q;
+    return (int)q;
+  };
+  const int tid = threadIdx.x;
+  int64_t it = bnd(s);
+  const int64_t it1 = bnd(s + 1);
+  while (it < it1) {
+    const int u = (int)(it / nk);
+    const int k0 = (int)(it - (int64_t)u * nk);
+    const int k1 = (int)min<int64_t>(nk, k0 + (it1 - it));
+    int ti, tj;
+    tile_of(p, p.sk_dp + u, ti, tj);
+    const int s0 = owner((int64_t)u * nk), s1 = owner((int64_t)u * nk + nk - 1);
+    if (s0 == s1) {  // the whole tile in this run
+      gemm_tile<ALAY, BLAY, EPI_STORE, TILE>(p, ti, tj, 0, smem);
+      __syncthreads();  // (its last slice is still being read when the next run stages)
+    } else {
+      gemm_tile<ALAY, BLAY, EPI_STORE, TILE>(p, ti, tj, 0, smem, k0 * BK, k1 * BK,
+                                             p.ws + (int64_t)(u + s) * TT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      unsigned int* flag = reinterpret_cast<unsigned int*>(smem);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(p.sk_cnt + u, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int last = t == s1 - s0 ? 1u : 0u;
+        if (last) {
+          __hip_atomic_store(p.sk_cnt + u, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        flag[0] = last;
+      }
+      __syncthreads();
+      const unsigned int last = __builtin_amdgcn_readfirstlane(flag[0]);
+      __syncthreads();  // (the next run's first LDS stores may overwrite the flag)
+      if (last) {
+        d4 acc[MI][MI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < MI; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
+        for (int q = s0; q <= s1; ++q) {  // block order: deterministic
+          const double* src = p.ws + (int64_t)(u + q) * TT + tid;
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < MI; ++ni)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[mi][ni][r] += src[((mi * MI + ni) * 4 + r) * 256];
+        }
+        store_acc<TILE>(p, ti, tj, 0, acc);
+      }
+    }
+    it += k1 - k0;
+  }
 }
 
 template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
-                                          double* smem) {
+                                          double* smem, int kb_o, int ke_o, double* part) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
   constexpr int WT = TILE / 2;           // per-wave sub-tile edge
@@ -179,7 +292,10 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
       break;
     default: break;
   }
-  if (p.ksplit > 1) {
+  if (kb_o >= 0) {  // a stream-K run: an explicit slice range of a uniform-K tile
+    kb = kb_o;
+    ke = ke_o;
+  } else if (p.ksplit > 1) {
     const int nk = ke > kb ? (ke - kb) / BK : 0;
     const int s = kslice, q = nk / p.ksplit, r = nk % p.ksplit;
     const int s0 = s * q + min(s, r), s1 = s0 + q + (s < r ? 1 : 0);
@@ -317,20 +433,16 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
 
   const int lrow = lane >> 4, lcol = lane & 15;
   if constexpr (EPI == EPI_STORE) {
-    double* Cb = p.C + (int64_t)kslice * p.c_kslice_stride;
+    if (part) {  // stream-K partial: this thread's accumulators, coalesced ([element][thread])
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = row0 + wr * WT + mi * 16 + lrow + 4 * r;
-        double* crow = Cb + (int64_t)row * p.ldc + col0 + wc * WT + lcol;
+        for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
-        for (int ni = 0; ni < MI; ++ni) {
-          double v = p.alpha * acc[mi][ni][r];
-          if (p.beta != 0.0) v = fma(p.beta, crow[ni * 16], v);
-          crow[ni * 16] = v;
-        }
-      }
+          for (int r = 0; r < 4; ++r) part[((mi * MI + ni) * 4 + r) * 256 + tid] = acc[mi][ni][r];
+      return;
+    }
+    store_acc<TILE>(p, ti, tj, kslice, acc);
   } else if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
     // out0[tj][row] = sum over this tile's columns of (alpha*acc)^2
     double* red = smem;  // [2 (wc)][TILE rows]
@@ -570,6 +682,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 }
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
+int g_stream_k = 1;   // GPS_OPT_STREAM_K (process-wide)
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
 static int small_wpt(int K) { return K >= 64 ? 4 : (K >= 32 ? 2 : 1); }
@@ -686,6 +799,20 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     tiles = (q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I) ? 8 * ((q.tiles_n + 7) / 8) * q.tiles_m
                                                           : 8 * ((q.tiles_m + 7) / 8) * q.tiles_n;
+  }
+  // stream-K tail (gemm_sk_block): a 128-tile EPI_STORE launch with uniform K ranges whose last
+  // round of workgroup slots would be at most 3/4 full runs that round's tiles as equal K runs
+  // over every slot instead
+  q.sk_dp = q.sk_wgs = 0;
+  if (g_stream_k && epi == EPI_STORE && tile == 128 && q.ksplit == 1 && q.sk_cnt && q.ws &&
+      q.sk_slots > 0 && q.tri == TRI_NONE && (q.lower_out || q.map_mode == 0 || q.map_mode == 2)) {
+    const int slots = q.sk_slots, rem = tiles % slots;
+    if (tiles >= slots && rem > 0 && 4 * rem <= 3 * slots && rem <= kStreamKTiles &&
+        (int64_t)(rem + slots) * 128 * 128 <= q.ws_cap && q.K / BK >= 2) {
+      q.sk_dp = tiles - rem;
+      q.sk_wgs = slots;
+      tiles = q.sk_dp + slots;
+    }
   }
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;

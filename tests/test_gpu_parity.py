@@ -707,6 +707,40 @@ def test_persistent_factorisation_load_groups_bitwise(gpu_ctx, n):
         assert np.array_equal(r.mu_loo, runs[0].mu_loo) and np.array_equal(r.var_loo, runs[0].var_loo)
 
 
+@pytest.mark.parametrize("n", [8192, 10000])
+def test_stream_k_tail(gpu_ctx, n):
+    """GPS_OPT_STREAM_K: the trailing-update SYRKs whose last round of workgroup slots would be
+    mostly empty (n = 8192: 528 tiles, 16 in the last round; n = 10 000: 820 and 3160-tile
+    levels) split that round into K runs combined in fixed order — the same products in another
+    summation order: agrees with one-workgroup-per-tile and with the oracle, and a refit is
+    bitwise identical."""
+    import gpscore
+    from gpscore import _lib
+    rng = np.random.default_rng(n)
+    d = 6
+    X = rng.standard_normal((n, d))
+    y = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n)
+    th = (0.2, np.log(1.7) * np.ones(d), np.log(0.02))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    runs = []
+    try:
+        for sk in (0, 1, 1):
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_STREAM_K, sk)
+            gp.fit(X, y, (0.5, np.log(0.9) * np.ones(d), np.log(0.05)))  # other values first
+            runs.append(gp.fit(X, y, th))
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_STREAM_K, 1)
+    r0, r1, r2 = runs
+    assert r1.objectives == r2.objectives
+    assert np.array_equal(r1.mu_loo, r2.mu_loo) and np.array_equal(r1.var_loo, r2.var_loo)
+    assert nrel(r1.mu_loo, r0.mu_loo) < 1e-11 and nrel(r1.var_loo, r0.var_loo) < 1e-11
+    for k in ("nlml", "loo_crps", "loo_logs", "logdet", "quad"):
+        assert abs(r1.objectives[k] - r0.objectives[k]) <= 1e-11 * max(1.0, abs(r0.objectives[k])), k
+    f = O.fast_full_fit(X, y, *th)
+    assert nrel(r1.mu_loo, f["loo_mu"]) < 1e-9 and nrel(r1.var_loo, f["loo_var"]) < 1e-9
+    assert abs(r1.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
+
+
 def test_persistent_factorisation_potrf_exports(gpu_ctx):
     """gps_potrf (L out of the persistent kernel's TRSM tasks and leaves) and the non-PD minor
     reported from inside a persistent block."""
