@@ -557,14 +557,17 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
     const std::vector<uint32_t> tl = dag_task_list(T);
     auto& e = ctx->dag_lists[T];
     HIPCHK(ensure(e.first, tl.size() * 4));
-    HIPCHK(hipMemcpy(e.first.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice));
+    // (stream-ordered, never the legacy stream: another context of this process may be
+    // capturing a graph on its own thread, and a legacy-stream call then fails)
+    HIPCHK(hipMemcpyAsync(e.first.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
     e.second = (int)tl.size();
   }
   if (dcnt && ctx->dag_cnt.cap < (size_t)dcnt * 4) {
     HIPCHK(hipStreamSynchronize(ctx->stream));  // no launch of this context still uses the old one
     HIPCHK(ensure(ctx->dag_cnt, std::max<size_t>((size_t)dcnt * 4, (size_t)1 << 20)));
-    HIPCHK(hipMemset(ctx->dag_cnt.p, 0, ctx->dag_cnt.cap));
-    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemsetAsync(ctx->dag_cnt.p, 0, ctx->dag_cnt.cap, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   auto eager = [&]() {
     ctx->sync_used = 0;
@@ -1157,7 +1160,8 @@ int gps_ctx_create(int device, gps_ctx** out) {
   HIPCHK(ensure(ctx->info, 16));
   HIPCHK(ensure(ctx->small, 256 * sizeof(double)));
   HIPCHK(ensure(ctx->sk_cnt, (size_t)kStreamKTiles * sizeof(int)));
-  HIPCHK(hipMemset(ctx->sk_cnt.p, 0, (size_t)kStreamKTiles * sizeof(int)));
+  HIPCHK(hipMemsetAsync(ctx->sk_cnt.p, 0, (size_t)kStreamKTiles * sizeof(int), ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   *out = ctx;
   return 0;
 }
@@ -1165,7 +1169,10 @@ int gps_ctx_create(int device, gps_ctx** out) {
 int gps_ctx_destroy(gps_ctx* ctx) {
   if (!ctx) return 0;
   (void)hipSetDevice(ctx->device);
-  (void)hipDeviceSynchronize();
+  // this context's own streams only (a device-wide synchronize would also wait on, and under a
+  // capture interfere with, other contexts of the process)
+  for (hipStream_t st : {ctx->stream, ctx->side, ctx->aux[0], ctx->aux[1]})
+    if (st) (void)hipStreamSynchronize(st);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   leave_local_group(ctx);
   for (DBuf* b : ctx_buffers(ctx)) release(*b);
