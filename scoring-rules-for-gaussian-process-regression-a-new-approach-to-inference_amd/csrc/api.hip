@@ -152,6 +152,7 @@ struct gps_ctx {
   DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
   DBuf ebuf_aux[3], bPIs, bRW;  // concurrent ES folds: work areas of the aux streams, C_f, r_f / w_f
   DBuf bfv;                       // sharded FITC block-LOO: row counts, then the fold values
+  DBuf rpart;                     // per-workgroup partials of the row finalisers (main stream)
   size_t bL_zeroed = 0;
   size_t lm_zeroed = 0, lb_zeroed = 0;
   int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
@@ -1127,7 +1128,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
                  &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->bfv, &ctx->dag_cnt, &ctx->sk_cnt};
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt};
 }
 
 extern "C" {
@@ -1464,6 +1465,13 @@ int gps_gemm(gps_ctx* ctx, int transA, int transB, int64_t M, int64_t N, int64_t
   return 0;
 }
 
+// scratch for the row finalisers' per-workgroup partials (kernels_vec.hip): nv per 256 rows
+static double* row_part(gps_ctx* ctx, int64_t rows, int nv) {
+  if (ensure(ctx->rpart, (size_t)(std::max<int64_t>(rows, 1) + 255) / 256 * nv * 8) != hipSuccess)
+    return nullptr;
+  return ctx->rpart.d();
+}
+
 int gps_scores(gps_ctx* ctx, const double* mu, const double* var, const double* y, int64_t nt,
                double ytr_mean, double ytr_var_unbiased, double out[GPS_N_SC]) {
   if (int rc = bind(ctx)) return rc;
@@ -1471,8 +1479,10 @@ int gps_scores(gps_ctx* ctx, const double* mu, const double* var, const double* 
   if (int rc = upload(ctx, ctx->t0, mu, nt, 1, nt)) return rc;
   if (int rc = upload(ctx, ctx->t1, var, nt, 1, nt)) return rc;
   if (int rc = upload(ctx, ctx->t2, y, nt, 1, nt)) return rc;
+  double* part = row_part(ctx, nt, 6);
+  ARGCHK(part != nullptr, "out of device memory");
   HIPCHK(launch_score_sums(ctx->t0.d(), ctx->t1.d(), ctx->t2.d(), (int)nt, ytr_mean,
-                           ytr_var_unbiased, ctx->small.d(), ctx->stream));
+                           ytr_var_unbiased, ctx->small.d(), part, ctx->stream));
   HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, 6 * 8, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   score_bundle(ctx->hsmall, (double)nt, out);
@@ -1698,8 +1708,10 @@ int gps_full_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
                            ctx->s2.d(), s));
     HIPCHK(launch_pred_finalize(ctx->s1.d(), ctx->s2.d(), (int)nt, ctx->th.sn2 + ctx->th.sf2,
                                 ctx->mu.d(), ctx->var.d(), s));
+    double* part = row_part(ctx, nt, 6);
+    ARGCHK(part != nullptr, "out of device memory");
     HIPCHK(launch_score_sums(ctx->mu.d(), ctx->var.d(), ctx->yt.d(), (int)nt, ctx->ytr_mean,
-                             ctx->ytr_var, ctx->small.d(), s));
+                             ctx->ytr_var, ctx->small.d(), part, s));
   }
   HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, 6 * 8, hipMemcpyDeviceToHost, s));
   if (mu) HIPCHK(hipMemcpyAsync(mu, ctx->mu.p, nt * 8, hipMemcpyDeviceToHost, s));
@@ -1983,11 +1995,13 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
   // q_i = ‖Lm⁻¹ k_i‖² (the remaining column tiles)
   if ((rc = fitc_rowsq_cols(ctx, ctx->Lm.d(), qn1, mp, s))) return rc;
-  HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->q.d(), s));
-  {
+  double* part = row_part(ctx, np, 2);
+  ARGCHK(part != nullptr, "out of device memory");
+  {  // q = Σ of the row-norm partials, fused with Λ (one thread per row, many workgroups)
     Prof pr(ctx, "fitc_lambda", 0, 0);
-    HIPCHK(launch_fitc_lambda(ctx->q.d(), ctx->fy.d(), (int)n, (int)np, th.sf2, th.sn2,
-                              ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal, s));
+    HIPCHK(launch_fitc_lambda(ctx->fslab.d(), np, (int)tm, ctx->fy.d(), (int)n, (int)np, th.sf2,
+                              th.sn2, ctx->q.d(), ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal,
+                              part, s));
   }
   {  // b_p = Kmnᵀ Λ⁻¹ y
     Prof pr(ctx, "colred_b", 0, 8.0 * np * mp);
@@ -2025,12 +2039,14 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     p.out0 = ctx->fslab.d(); p.ld_out = np;
     p.w = ctx->c.d(); p.out1 = ctx->g.d();
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ_DOT, p))) return rc;
-    HIPCHK(launch_slab_sum(ctx->fslab.d(), np, (int)tm, np, nullptr, ctx->r.d(), s));
   }
-  {
+  {  // r = Σ of the row-norm partials, fused with the LOO terms
+    part = row_part(ctx, np, 2);
+    ARGCHK(part != nullptr, "out of device memory");
     Prof pr(ctx, "fitc_loo", 0, 0);
-    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n,
-                           ctx->fmu_loo.d(), ctx->fvar_loo.d(), scal + 2, s));
+    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->fslab.d(), np, (int)tm, ctx->g.d(),
+                           (int)n, (int)np, ctx->r.d(), ctx->fmu_loo.d(), ctx->fvar_loo.d(),
+                           scal + 2, part, s));
   }
   if ((rc = allreduce_sum(ctx, scal + 2, 2, s))) return rc;
   // the pre-pass reads the test inputs: it is done before this call returns (it finished long
@@ -2779,9 +2795,11 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
     if (nt > 0)  // a rank may hold no test rows; its zero score partials still join the sum
       HIPCHK(launch_fitc_pred_finalize(ctx->qm.d(), ctx->qb.d(), (int)nt, th.sn2 + th.sf2,
                                        ctx->fvar.d(), s));
+    double* part = row_part(ctx, nt, 6);
+    ARGCHK(part != nullptr, "out of device memory");
     if (nt > 0)
       HIPCHK(launch_score_sums(ctx->fmu.d(), ctx->fvar.d(), ctx->fyt.d(), (int)nt, ctx->f_ytr_mean,
-                               ctx->f_ytr_var, sums, s));
+                               ctx->f_ytr_var, sums, part, s));
     else
       HIPCHK(hipMemsetAsync(sums, 0, 6 * 8, s));
   }

@@ -240,16 +240,22 @@ hipError_t launch_pred_finalize(const double* s1, const double* s2, int nt, doub
 hipError_t launch_fitc_pred_finalize(const double* qm, const double* qb, int nt, double base_var,
                                      double* var, hipStream_t s);
 // sums: [crps, logs, msll, sq_err, sq_err_trivial, cover]
+// (part: scratch of ⌈nt/256⌉·6 doubles for the per-workgroup partials)
 hipError_t launch_score_sums(const double* mu, const double* var, const double* y, int nt,
-                             double ytr_mean, double ytr_var, double* sums, hipStream_t s);
-// FITC: λ_i = sf2 − q_i + σ² (real rows), 1 on pad rows; inv_lam = 1/λ; ys = y/λ;
-// scalars: [Σ log λ, Σ y²/λ]
-hipError_t launch_fitc_lambda(const double* q, const double* y, int n, int n_pad, double sf2,
-                              double sn2, double* lam, double* inv_lam, double* ys,
-                              double* scal, hipStream_t s);
-// FITC LOO sums: d = 1/λ − r/λ², α = (y − g)/λ → μ, σ²; sums [Σ crps, Σ logs]
-hipError_t launch_fitc_loo(const double* y, const double* lam, const double* r, const double* g,
-                           int n, double* mu_loo, double* var_loo, double* sums, hipStream_t s);
+                             double ytr_mean, double ytr_var, double* sums, double* part,
+                             hipStream_t s);
+// FITC: q_i = Σ_t slab[t·ld + i] (nslab row-norm partials), λ_i = sf2 − q_i + σ² (real rows),
+// 1 on pad rows; inv_lam = 1/λ; ys = y/λ; scalars: [Σ log λ, Σ y²/λ]
+// (part: scratch of ⌈n_pad/256⌉·2 doubles)
+hipError_t launch_fitc_lambda(const double* slab, int64_t ld, int nslab, const double* y, int n,
+                              int n_pad, double sf2, double sn2, double* q, double* lam,
+                              double* inv_lam, double* ys, double* scal, double* part,
+                              hipStream_t s);
+// FITC LOO: r_i = Σ_t slab[t·ld + i], d = 1/λ − r/λ², α = (y − g)/λ → μ, σ²; sums [Σ crps, Σ logs]
+hipError_t launch_fitc_loo(const double* y, const double* lam, const double* slab, int64_t ld,
+                           int nslab, const double* g, int n, int n_pad, double* r,
+                           double* mu_loo, double* var_loo, double* sums, double* part,
+                           hipStream_t s);
 // small dense triangular mat-vec on the device: y = op(L) x with L lower (n_pad)
 hipError_t launch_trmv_lower(const double* L, int64_t ldl, const double* x, double* y,
                              int n_pad, int trans, hipStream_t s);

@@ -60,6 +60,9 @@ __global__ __launch_bounds__(256) void colred_kernel(const double* __restrict__ 
   int r0 = chunk * CR_ROWS, r1 = min(rows, r0 + CR_ROWS);
   if (lower) r0 = max(r0, (c / GPS_TILE) * GPS_TILE);
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  // (unrolled so 8 rows' loads are in flight ahead of the in-order FMAs: one memory latency
+  // per 8 rows instead of per row — the m×m passes of the FITC path have only a few chunks)
+#pragma unroll 8
   for (int r = r0; r < r1; ++r) {
     double2 v = *reinterpret_cast<const double2*>(M + (int64_t)r * ldm + c);
     if (rowscale) {
@@ -103,7 +106,7 @@ hipError_t launch_colred(const double* M, int64_t ldm, int rows, int cols, int l
                          const double* w, const double* rowscale, double* s1, double* s2,
                          double* slab, hipStream_t s) {
   if ((cols & 1) || (ldm & 1)) return hipErrorInvalidValue;
-  const int nchunk = (rows + CR_ROWS - 1) / CR_ROWS;
+  const int nchunk = (rows + CR_ROWS - 1) / CR_ROWS;  // (CR_ROWS rows per chunk: see the kernel)
   double* slab1 = s1 ? slab : nullptr;
   double* slab2 = s2 ? slab + (int64_t)nchunk * cols : nullptr;
   hipLaunchKernelGGL(colred_kernel, dim3((cols + CR_COLS - 1) / CR_COLS, nchunk), dim3(256), 0, s,
@@ -242,6 +245,27 @@ hipError_t launch_full_loo(const double* y, const double* alpha, const double* d
   return hipGetLastError();
 }
 
+// ------------------------------------------------------ two-level row sums
+// The row finalisers below run one thread per row over many workgroups (a single workgroup
+// walking 40k-200k rows took 30-105 µs of a FITC unit's critical path); each workgroup writes
+// its block_sum partials to part[block·NV + q] and this one-workgroup kernel adds them in block
+// order through a fixed tree — deterministic, like every reduction here.
+template <int NV>
+__global__ __launch_bounds__(1024) void partials_sum_kernel(const double* __restrict__ part,
+                                                            int nblk, double* __restrict__ out) {
+  __shared__ double sh[NV * 16];
+  double v[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) v[q] = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 1024)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] += part[(int64_t)b * NV + q];
+  block_sum<NV>(v, sh);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) out[q] = v[q];
+}
+
 // --------------------------------------------------------------- predictive
 __global__ __launch_bounds__(256) void pred_finalize_kernel(const double* __restrict__ s1,
                                                             const double* __restrict__ s2, int nt,
@@ -275,56 +299,64 @@ hipError_t launch_fitc_pred_finalize(const double* qm, const double* qb, int nt,
 }
 
 // sums: [Σcrps, Σlogs, Σmsll, Σ(μ−y)², Σ(ȳtr−y)², Σcover]  (KF:276-292, 110-134)
-__global__ __launch_bounds__(1024) void score_sums_kernel(const double* __restrict__ mu,
-                                                          const double* __restrict__ var,
-                                                          const double* __restrict__ y, int nt,
-                                                          double ytr_mean, double ytr_var,
-                                                          double* __restrict__ sums) {
+__global__ __launch_bounds__(256) void score_rows_kernel(const double* __restrict__ mu,
+                                                         const double* __restrict__ var,
+                                                         const double* __restrict__ y, int nt,
+                                                         double ytr_mean, double ytr_var,
+                                                         double* __restrict__ part) {
   __shared__ double sh[6 * 16];
   double v[6] = {0, 0, 0, 0, 0, 0};
-  const double triv_c = 0.5 * log(6.28318530717958647692 * ytr_var);
-  for (int j = threadIdx.x; j < nt; j += blockDim.x) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < nt) {
+    const double triv_c = 0.5 * log(6.28318530717958647692 * ytr_var);
     const double m = mu[j], c = var[j], t = y[j];
-    v[0] += crps_term(m, c, t);
+    v[0] = crps_term(m, c, t);
     const double ls = logs_term(m, c, t);
-    v[1] += ls;
+    v[1] = ls;
     const double e0 = t - ytr_mean;
-    v[2] += ls - (triv_c + e0 * e0 / (2.0 * ytr_var));
-    v[3] += (m - t) * (m - t);
-    v[4] += e0 * e0;
+    v[2] = ls - (triv_c + e0 * e0 / (2.0 * ytr_var));
+    v[3] = (m - t) * (m - t);
+    v[4] = e0 * e0;
     const double sd = sqrt(c);
-    v[5] += ((m + 2.0 * sd - t) > 0.0 && (t - (m - 2.0 * sd)) > 0.0) ? 1.0 : 0.0;
+    v[5] = ((m + 2.0 * sd - t) > 0.0 && (t - (m - 2.0 * sd)) > 0.0) ? 1.0 : 0.0;
   }
   block_sum<6>(v, sh);
   if (threadIdx.x == 0)
-    for (int q = 0; q < 6; ++q) sums[q] = v[q];
+    for (int q = 0; q < 6; ++q) part[(int64_t)blockIdx.x * 6 + q] = v[q];
 }
 hipError_t launch_score_sums(const double* mu, const double* var, const double* y, int nt,
-                             double ytr_mean, double ytr_var, double* sums, hipStream_t s) {
-  hipLaunchKernelGGL(score_sums_kernel, dim3(1), dim3(1024), 0, s, mu, var, y, nt, ytr_mean,
-                     ytr_var, sums);
+                             double ytr_mean, double ytr_var, double* sums, double* part,
+                             hipStream_t s) {
+  const int nblk = std::max(1, (nt + 255) / 256);
+  hipLaunchKernelGGL(score_rows_kernel, dim3(nblk), dim3(256), 0, s, mu, var, y, nt, ytr_mean,
+                     ytr_var, part);
+  hipLaunchKernelGGL(partials_sum_kernel<6>, dim3(1), dim3(1024), 0, s, part, nblk, sums);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------- FITC
-__global__ __launch_bounds__(1024) void fitc_lambda_kernel(const double* __restrict__ q,
-                                                           const double* __restrict__ y, int n,
-                                                           int n_pad, double sf2, double sn2,
-                                                           double* __restrict__ lam,
-                                                           double* __restrict__ inv_lam,
-                                                           double* __restrict__ ys,
-                                                           double* __restrict__ scal) {
+// q_i = Σ_t slab_t[i] (the row-norm GEMM's per-column-tile partials, summed in tile order as
+// slab_sum_kernel does), then Λ: λ_i = sf2 − q_i + σ² (K20:225-228), 1/λ, y/λ; partial sums
+// [Σ log λ, Σ y²/λ] per workgroup
+__global__ __launch_bounds__(256) void fitc_lambda_rows_kernel(
+    const double* __restrict__ slab, int64_t ld, int nslab, const double* __restrict__ y, int n,
+    int n_pad, double sf2, double sn2, double* __restrict__ q, double* __restrict__ lam,
+    double* __restrict__ inv_lam, double* __restrict__ ys, double* __restrict__ part) {
   __shared__ double sh[2 * 16];
   double v[2] = {0.0, 0.0};
-  for (int i = threadIdx.x; i < n_pad; i += blockDim.x) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n_pad) {
+    double qi = 0.0;
+    for (int t = 0; t < nslab; ++t) qi += slab[(int64_t)t * ld + i];
+    q[i] = qi;
     if (i < n) {
-      const double l = sf2 - q[i] + sn2;  // G = diag(K_ff − Q_ff + σ²I), K20:225-228
+      const double l = sf2 - qi + sn2;
       const double il = 1.0 / l;
       lam[i] = l;
       inv_lam[i] = il;
       ys[i] = y[i] * il;
-      v[0] += log(l);
-      v[1] = fma(y[i] * y[i], il, v[1]);
+      v[0] = log(l);
+      v[1] = y[i] * y[i] * il;
     } else {
       lam[i] = 1.0;
       inv_lam[i] = 0.0;  // padded rows carry no weight in B = Kmnᵀ Λ⁻¹ Knm
@@ -333,49 +365,60 @@ __global__ __launch_bounds__(1024) void fitc_lambda_kernel(const double* __restr
   }
   block_sum<2>(v, sh);
   if (threadIdx.x == 0) {
-    scal[0] = v[0];
-    scal[1] = v[1];
+    part[(int64_t)blockIdx.x * 2] = v[0];
+    part[(int64_t)blockIdx.x * 2 + 1] = v[1];
   }
 }
-hipError_t launch_fitc_lambda(const double* q, const double* y, int n, int n_pad, double sf2,
-                              double sn2, double* lam, double* inv_lam, double* ys, double* scal,
+hipError_t launch_fitc_lambda(const double* slab, int64_t ld, int nslab, const double* y, int n,
+                              int n_pad, double sf2, double sn2, double* q, double* lam,
+                              double* inv_lam, double* ys, double* scal, double* part,
                               hipStream_t s) {
-  hipLaunchKernelGGL(fitc_lambda_kernel, dim3(1), dim3(1024), 0, s, q, y, n, n_pad, sf2, sn2, lam,
-                     inv_lam, ys, scal);
+  const int nblk = std::max(1, (n_pad + 255) / 256);
+  hipLaunchKernelGGL(fitc_lambda_rows_kernel, dim3(nblk), dim3(256), 0, s, slab, ld, nslab, y, n,
+                     n_pad, sf2, sn2, q, lam, inv_lam, ys, part);
+  hipLaunchKernelGGL(partials_sum_kernel<2>, dim3(1), dim3(1024), 0, s, part, nblk, scal);
   return hipGetLastError();
 }
 
-// sums: [Σcrps, Σlogs] over this shard's rows
-__global__ __launch_bounds__(1024) void fitc_loo_kernel(const double* __restrict__ y,
-                                                        const double* __restrict__ lam,
-                                                        const double* __restrict__ r,
-                                                        const double* __restrict__ g, int n,
-                                                        double* __restrict__ mu_loo,
-                                                        double* __restrict__ var_loo,
-                                                        double* __restrict__ sums) {
+// r_i = Σ_t slab_t[i] (the Lb row-norm partials), then the LOO terms: d = 1/λ − r/λ²,
+// α = (y − g)/λ → μ = y − α/d, σ² = 1/d (K20:231-232); partial sums [Σ crps, Σ logs]
+__global__ __launch_bounds__(256) void fitc_loo_rows_kernel(
+    const double* __restrict__ y, const double* __restrict__ lam, const double* __restrict__ slab,
+    int64_t ld, int nslab, const double* __restrict__ g, int n, int n_pad, double* __restrict__ r,
+    double* __restrict__ mu_loo, double* __restrict__ var_loo, double* __restrict__ part) {
   __shared__ double sh[2 * 16];
   double v[2] = {0.0, 0.0};
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const double il = 1.0 / lam[i];
-    const double d = il - r[i] * il * il;   // diag((Q+Λ)⁻¹), Woodbury
-    const double a = (y[i] - g[i]) * il;    // ((Q+Λ)⁻¹ y)_i
-    const double m = y[i] - a / d;          // K20:231
-    const double c = 1.0 / d;               // K20:232
-    mu_loo[i] = m;
-    var_loo[i] = c;
-    v[0] += crps_term(m, c, y[i]);
-    v[1] += logs_term(m, c, y[i]);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n_pad) {
+    double ri = 0.0;
+    for (int t = 0; t < nslab; ++t) ri += slab[(int64_t)t * ld + i];
+    r[i] = ri;
+    if (i < n) {
+      const double il = 1.0 / lam[i];
+      const double d = il - ri * il * il;   // diag((Q+Λ)⁻¹), Woodbury
+      const double a = (y[i] - g[i]) * il;  // ((Q+Λ)⁻¹ y)_i
+      const double m = y[i] - a / d;        // K20:231
+      const double c = 1.0 / d;             // K20:232
+      mu_loo[i] = m;
+      var_loo[i] = c;
+      v[0] = crps_term(m, c, y[i]);
+      v[1] = logs_term(m, c, y[i]);
+    }
   }
   block_sum<2>(v, sh);
   if (threadIdx.x == 0) {
-    sums[0] = v[0];
-    sums[1] = v[1];
+    part[(int64_t)blockIdx.x * 2] = v[0];
+    part[(int64_t)blockIdx.x * 2 + 1] = v[1];
   }
 }
-hipError_t launch_fitc_loo(const double* y, const double* lam, const double* r, const double* g,
-                           int n, double* mu_loo, double* var_loo, double* sums, hipStream_t s) {
-  hipLaunchKernelGGL(fitc_loo_kernel, dim3(1), dim3(1024), 0, s, y, lam, r, g, n, mu_loo, var_loo,
-                     sums);
+hipError_t launch_fitc_loo(const double* y, const double* lam, const double* slab, int64_t ld,
+                           int nslab, const double* g, int n, int n_pad, double* r,
+                           double* mu_loo, double* var_loo, double* sums, double* part,
+                           hipStream_t s) {
+  const int nblk = std::max(1, (n_pad + 255) / 256);
+  hipLaunchKernelGGL(fitc_loo_rows_kernel, dim3(nblk), dim3(256), 0, s, y, lam, slab, ld, nslab, g,
+                     n, n_pad, r, mu_loo, var_loo, part);
+  hipLaunchKernelGGL(partials_sum_kernel<2>, dim3(1), dim3(1024), 0, s, part, nblk, sums);
   return hipGetLastError();
 }
 
