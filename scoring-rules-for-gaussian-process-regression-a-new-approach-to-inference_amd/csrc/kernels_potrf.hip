@@ -592,8 +592,12 @@ __device__ __attribute__((noinline)) void tile_task(const double* Ap, int64_t ld
         for (int ni = 0; ni < 4; ++ni)
           acc[mi][ni][r] = ld64(rc, (uint32_t)(((int64_t)(wr * 32 + mi * 16 + lrow + 4 * r) * ldc +
                                                 wc * 64 + ni * 16 + lcol) * 8));
-    dv2 sa[2], sb[4];
-    auto load = [&](int k0) {
+    // two slices in flight in registers: one compute phase (~0.9 µs with one wave per SIMD) does
+    // not cover a coherent load's fabric latency, two nearly do
+    dv2 sa2[2][2], sb2[2][4];
+    auto load = [&](int k0, int set) {
+      dv2* sa = sa2[set];
+      dv2* sb = sb2[set];
 #pragma unroll
       for (int q = 0; q < 2; ++q) sa[q] = ld128(ra, (uint32_t)(((int64_t)ai * lda + k0 + ak + 2 * q) * 8));
       if constexpr (BT) {
@@ -606,7 +610,9 @@ __device__ __attribute__((noinline)) void tile_task(const double* Ap, int64_t ld
           sb[q] = ld128(rb, (uint32_t)(((int64_t)(k0 + bk) * ldb + bj + 2 * q) * 8));
       }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int set) {
+      const dv2* sa = sa2[set];
+      const dv2* sb = sb2[set];
       double* As = smem + buf * TSTAGE;
       double* Bs = As + 16 * TLS;
 #pragma unroll
@@ -642,13 +648,15 @@ __device__ __attribute__((noinline)) void tile_task(const double* Ap, int64_t ld
           for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4::mfma(a[mi], b[ni], acc[mi][ni]);
       }
     };
-    load(0);
-    store(0);
+    load(0, 0);
+    load(16, 1);
+    store(0, 0);
     __syncthreads();
-    for (int sl = 0; sl < 7; ++sl) {
-      load(16 * (sl + 1));
+#pragma unroll
+    for (int sl = 0; sl < 7; ++sl) {  // slice sl+1 sits in register set (sl+1)&1
+      if (sl + 2 < 8) load(16 * (sl + 2), sl & 1);
       compute(sl & 1);
-      store((sl + 1) & 1);
+      store((sl + 1) & 1, (sl + 1) & 1);
       __syncthreads();
     }
     compute(1);
