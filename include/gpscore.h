@@ -106,9 +106,6 @@ enum {
                              most 3/4 full splits that round's tiles into equal K runs over every
                              slot (in-launch fixed-order combine); 0: one workgroup per tile.
                              Process-wide. */
-  GPS_OPT_DAG_WHOLE = 19, /* 1 (default): the persistent factorisation runs the off-diagonal
-                             trailing updates as whole-tile tasks (one workgroup per 128×128 tile,
-                             LDS-staged); 0: as 4 row strips each, like every other task */
   GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
                              flight per load group (2, 3 (default) or 4).  Same values bitwise. */
 };

@@ -104,8 +104,7 @@ struct gps_ctx {
   bool dag = true;                     // GPS_OPT_DAG: persistent factorisation of the bottom blocks
   int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
-  int dag_whole = 1;                   // GPS_OPT_DAG_WHOLE
-  std::map<int, std::pair<DBuf, int>> dag_lists;  // per (2T + whole): device task list, length
+  std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
   int64_t dag_cnt_used = 0;
@@ -428,7 +427,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     return 0;
   }
   if (dag_block(ctx, nb)) {  // the whole block in one persistent launch (kernels_potrf.hip)
-    auto it = ctx->dag_lists.find(2 * nb + ctx->dag_whole);
+    auto it = ctx->dag_lists.find(nb);
     const int64_t need = dag_cnt_ints(nb);
     if (it == ctx->dag_lists.end() || ctx->dag_cnt_used + need > (int64_t)(ctx->dag_cnt.cap / 4))
       return fail(ctx, -2, "persistent factorisation: task list / counters not prepared");
@@ -555,10 +554,9 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   int64_t dcnt = 0;
   dag_blocks(ctx, n_pad / GPS_TILE, dsizes, dcnt);
   for (int T : dsizes) {
-    const int key = 2 * T + ctx->dag_whole;  // (block size, whole-tile tasks)
-    if (ctx->dag_lists.count(key)) continue;
-    const std::vector<uint32_t> tl = dag_task_list(T, 1, ctx->dag_whole != 0);
-    auto& e = ctx->dag_lists[key];
+    if (ctx->dag_lists.count(T)) continue;
+    const std::vector<uint32_t> tl = dag_task_list(T);
+    auto& e = ctx->dag_lists[T];
     HIPCHK(ensure(e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
     // capturing a graph on its own thread, and a legacy-stream call then fails)
@@ -595,7 +593,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
-      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_whole, (uintptr_t)ctx->dag_cnt.p};
+      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_cnt.p};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
@@ -1241,7 +1239,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
     case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;
     case GPS_OPT_DAG: ctx->dag = value != 0; return 0;
-    case GPS_OPT_DAG_WHOLE: ctx->dag_whole = value != 0; return 0;
     case GPS_OPT_DAG_GROUP:
       ARGCHK(value >= 2 && value <= 4, "GPS_OPT_DAG_GROUP must be 2, 3 or 4");
       ctx->dag_group = value;

@@ -200,8 +200,7 @@ struct DagParams {
   int group = 3;                   // 16-deep operand chunks per load group of a strip task (2..4)
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
-// tiles: the off-diagonal trailing updates as whole-tile tasks (word bit 7) instead of 4 strips
-std::vector<uint32_t> dag_task_list(int T, int order = 1, bool tiles = true);
+std::vector<uint32_t> dag_task_list(int T, int order = 1);
 inline int64_t dag_cnt_ints(int T) { return (16 + 2 * (int64_t)T * T + 63) / 64 * 64; }
 
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)

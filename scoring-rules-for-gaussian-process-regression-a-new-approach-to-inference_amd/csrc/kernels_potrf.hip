@@ -553,125 +553,6 @@ __device__ __forceinline__ void run_strip(const Strip& s) {
       }
 }
 
-// Whole-tile task (the bulk of the trailing updates: UPD(i,j,k) with i ≠ j, UPDX(i,k,j) with
-// j ≠ k): C (128×128, in place) += alpha · A·op(B) over K = 128 on one workgroup, the GEMM kernel's
-// structure (kernels_gemm.hip): 4 waves of 64×64 (4×4 blocks of v_mfma_f64_16x16x4), 16-deep K
-// slices double-buffered through LDS (k-major images, row stride 144 doubles), the next slice in
-// registers while this one is multiplied — with the coherent (sc1) loads and write-through
-// stores of the hand-off protocol.  The accumulators start from C itself (acc = C + alpha·A·B:
-// the summation order of a sequential in-place update), alpha folded into A's LDS image.  A is
-// i-major [i][k] (L); B is [j][k] (BT, UPD: L_jk) or [k][j] (UPDX: X_jk).  One task per tile
-// instead of 4 strip tasks: the fixed per-task cost (queue fetch, counter poll, operand fabric
-// latency, drain — ~8 µs against a strip's 3.4 µs of MFMA) is paid once per 14 µs of MFMA, which
-// is what lets the persistent launch take larger blocks (profiles/r3_dag_tile_*).
-constexpr int TLS = 144;             // LDS row stride of a tile-task image (doubles)
-constexpr int TSTAGE = 2 * 16 * TLS;  // one stage: A image (64 rows used) + B image
-// (the tile runs as two 64-row halves, each wave a 32×64 block: 64 accumulator VGPRs instead of
-// 128, so the path fits beside the leaf's registers without spills)
-template <bool BT>
-__device__ __attribute__((noinline)) void tile_task(const double* Ap, int64_t lda, const double* Bp,
-                                          int64_t ldb, double* Cp, int64_t ldc, double alpha,
-                                          double* smem) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1, lrow = lane >> 4, lcol = lane & 15;
-  const __amdgpu_buffer_rsrc_t rb = rsrc(Bp, (uint32_t)(128 * ldb * 8));
-  // staging: A half (64 rows) thread → row tid/4, k quarter (tid&3)·4; B as [j][k] (BT): row
-  // tid/2, k-half (tid&1)·8; B as [k][j]: k = tid/16, j = (tid%16)·8
-  const int ai = tid >> 2, ak = (tid & 3) * 4;
-  const int bi = tid >> 1, bkh = (tid & 1) * 8;
-  const int bk = tid >> 4, bj = (tid & 15) * 8;
-  for (int h = 0; h < 2; ++h) {
-    const __amdgpu_buffer_rsrc_t ra = rsrc(Ap + (int64_t)64 * h * lda, (uint32_t)(64 * lda * 8));
-    const __amdgpu_buffer_rsrc_t rc = rsrc(Cp + (int64_t)64 * h * ldc, (uint32_t)(64 * ldc * 8));
-    d4 acc[2][4];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni][r] = ld64(rc, (uint32_t)(((int64_t)(wr * 32 + mi * 16 + lrow + 4 * r) * ldc +
-                                                wc * 64 + ni * 16 + lcol) * 8));
-    // two slices in flight in registers: one compute phase (~0.9 µs with one wave per SIMD) does
-    // not cover a coherent load's fabric latency, two nearly do
-    dv2 sa2[2][2], sb2[2][4];
-    auto load = [&](int k0, int set) {
-      dv2* sa = sa2[set];
-      dv2* sb = sb2[set];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) sa[q] = ld128(ra, (uint32_t)(((int64_t)ai * lda + k0 + ak + 2 * q) * 8));
-      if constexpr (BT) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          sb[q] = ld128(rb, (uint32_t)(((int64_t)bi * ldb + k0 + bkh + 2 * q) * 8));
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          sb[q] = ld128(rb, (uint32_t)(((int64_t)(k0 + bk) * ldb + bj + 2 * q) * 8));
-      }
-    };
-    auto store = [&](int buf, int set) {
-      const dv2* sa = sa2[set];
-      const dv2* sb = sb2[set];
-      double* As = smem + buf * TSTAGE;
-      double* Bs = As + 16 * TLS;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        As[(ak + 2 * q) * TLS + ai] = alpha * sa[q].x;
-        As[(ak + 2 * q + 1) * TLS + ai] = alpha * sa[q].y;
-      }
-      if constexpr (BT) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          Bs[(bkh + 2 * q) * TLS + bi] = sb[q].x;
-          Bs[(bkh + 2 * q + 1) * TLS + bi] = sb[q].y;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) *reinterpret_cast<dv2*>(&Bs[bk * TLS + bj + 2 * q]) = sb[q];
-      }
-    };
-    auto compute = [&](int buf) {
-      const double* As = smem + buf * TSTAGE;
-      const double* Bs = As + 16 * TLS;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int krow = (kk * 4 + lrow) * TLS + lcol;
-        double a[2], b[4];
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) a[mi] = As[krow + wr * 32 + mi * 16];
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b[ni] = Bs[krow + wc * 64 + ni * 16];
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = v4::mfma(a[mi], b[ni], acc[mi][ni]);
-      }
-    };
-    load(0, 0);
-    load(16, 1);
-    store(0, 0);
-    __syncthreads();
-#pragma unroll
-    for (int sl = 0; sl < 7; ++sl) {  // slice sl+1 sits in register set (sl+1)&1
-      if (sl + 2 < 8) load(16 * (sl + 2), sl & 1);
-      compute(sl & 1);
-      store((sl + 1) & 1, (sl + 1) & 1);
-      __syncthreads();
-    }
-    compute(1);
-    __syncthreads();  // (the next half's first stage overwrites buffer 0)
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          st64(rc, (uint32_t)(((int64_t)(wr * 32 + mi * 16 + lrow + 4 * r) * ldc + wc * 64 + ni * 16 + lcol) * 8),
-               acc[mi][ni][r]);
-  }
-}
-
 // Counters: cnt[0] the queue head, cnt[1] the workgroups out, cnt[16..] the arrival counters —
 // zero at launch, zero again when the last workgroup leaves.
 // TRACE: per queue slot t, trace[4t..4t+3] = {fetched, inputs ready, outputs drained} in 100 MHz
@@ -697,14 +578,13 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   // that only lane 0 takes, and the SIMT lowering then loops the other lanes over a stale task.
   int* out = nullptr;
   int* out2 = nullptr;
-  int inc = 1;
   unsigned long long* trow = nullptr;  // TRACE: the current slot's record
   for (;;) {
     if (tid == 0) {
       if constexpr (TRACE) {  // (the previous task's "done" stamp lives here for the same reason)
         if (trow) trow[2] = __builtin_amdgcn_s_memrealtime();
       }
-      if (out) __hip_atomic_fetch_add(out, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (out) __hip_atomic_fetch_add(out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (out2) __hip_atomic_fetch_add(out2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int t = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sh[0] = t < p.ntasks ? p.tasks[t] : 0xffffffffu;
@@ -725,7 +605,6 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
     }
     const int type = w & 7, part = (w >> 3) & 3, ti = (w >> 8) & 255, tj = (w >> 16) & 255,
               tk = (w >> 24) & 255;
-    const bool whole = (w >> 7) & 1;  // a whole-tile task (tile_task): its arrival counts NP
     // ---- the counts this task needs (see the header); up to three, polled by wave 0 (every
     //      lane loads the same word; the exit test is taken on lane 0's view)
     if (wave == 0) {
@@ -779,19 +658,7 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
     }
     const int64_t lda = p.lda, ldl = p.ldl;
     out2 = nullptr;
-    inc = whole ? NP : 1;
-    if (whole) {  // UPD(i,j,k), i ≠ j: A_ij −= L_ik L_jkᵀ;  UPDX(i,k,j), j ≠ k: S_ik += L_ij X_jk
-      const int64_t R = 128 * (int64_t)ti, J = 128 * (int64_t)tj, K = 128 * (int64_t)tk;
-      if (type == 2) {
-        tile_task<true>(p.A + R * lda + K, lda, p.A + J * lda + K, lda, p.A + R * lda + J, lda,
-                        -1.0, S);
-        out = acnt + ti * T + tj;
-      } else {
-        tile_task<false>(p.A + R * lda + J, lda, p.Linv + J * ldl + K, ldl, p.Linv + R * ldl + K,
-                         ldl, 1.0, S);
-        out = xcnt + ti * T + tk;
-      }
-    } else if (type == 0) {
+    if (type == 0) {
       const int64_t o = (int64_t)128 * ti;
       v4::leaf_body<true>(p.A + o * lda + o, lda, p.Linv + o * ldl + o, ldl,
                           p.Lout ? p.Lout + o * p.ldlo + o : nullptr, p.ldlo, p.logdiag + o,
@@ -894,8 +761,8 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
 //            the block, leaf 38, strip 9, hand-off 1: the durations the r3 trace measured), so the
 //            updates that feed the next leaves overtake the bulk of the trailing update (the first
 //            leaves waited 20-26 µs behind it).
-// Word: type | part << 3 | whole << 7 | i << 8 | j << 16 | k << 24.
-std::vector<uint32_t> dag_task_list(int T, int order, bool tiles) {
+// Word: type | part << 3 | i << 8 | j << 16 | k << 24.
+std::vector<uint32_t> dag_task_list(int T, int order) {
   struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0, rank = 0.0; };
   std::vector<Task> tk;
   std::vector<int> leaf(T), trsm(T * T, -1), fin(T * T, -1);
@@ -930,16 +797,12 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool tiles) {
   std::vector<int> indeg(n, 0);
   for (int t = 0; t < n; ++t)
     for (int d : tk[t].deps) { succ[d].push_back(t); ++indeg[t]; }
-  // whole-tile tasks (one workgroup, tile_task) for the off-diagonal trailing updates
-  auto whole = [&](const Task& t) {
-    return tiles && ((t.type == 2 && t.i != t.j) || (t.type == 3 && t.j != t.k));
-  };
   if (order == 0) {
     auto dur = [&](const Task& t) { return t.type == 0 ? 36.0 : 4.0; };
     for (int t = 0; t < n; ++t)  // generation order is topological
       for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
   } else {
-    auto dur = [&](const Task& t) { return t.type == 0 ? 38.0 : whole(t) ? 18.0 : 9.0; };
+    auto dur = [&](const Task& t) { return t.type == 0 ? 38.0 : 9.0; };
     for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
       double m = 0.0;
       for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + 1.0);
@@ -956,11 +819,10 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool tiles) {
     const int t = ready.top().second;
     ready.pop();
     const Task& x = tk[t];
-    const bool w1 = whole(x);
-    const int parts = x.type == 0 || w1 ? 1 : dag::NP;
+    const int parts = x.type == 0 ? 1 : dag::NP;
     for (int q = 0; q < parts; ++q)
-      out.push_back((uint32_t)x.type | (uint32_t)q << 3 | (w1 ? 1u << 7 : 0u) | (uint32_t)x.i << 8 |
-                    (uint32_t)x.j << 16 | (uint32_t)x.k << 24);
+      out.push_back((uint32_t)x.type | (uint32_t)q << 3 | (uint32_t)x.i << 8 | (uint32_t)x.j << 16 |
+                    (uint32_t)x.k << 24);
     for (int s2 : succ[t])
       if (!--indeg[s2]) ready.push({tk[s2].est, s2});
   }

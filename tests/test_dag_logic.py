@@ -24,14 +24,12 @@ def task_list(T):
     assert n > 0
     out = (ctypes.c_uint32 * n)()
     assert lib.gps_dag_task_list(T, ctypes.cast(out, ctypes.c_void_p), n) == n
-    # (type, part, i, j, k, whole): whole-tile tasks (bit 7) count NP_ arrivals at once
-    return [(w & 7, (w >> 3) & 3, (w >> 8) & 255, (w >> 16) & 255, (w >> 24) & 255, (w >> 7) & 1)
-            for w in out]
+    return [(w & 7, (w >> 3) & 3, (w >> 8) & 255, (w >> 16) & 255, (w >> 24) & 255) for w in out]
 
 
 def needs(t, T):
     """(counter array, i, j, threshold) pairs a strip task polls (the kernel's switch)."""
-    typ, _, i, j, k = t[:5]
+    typ, _, i, j, k = t
     if typ == 0:
         return [("a", i, i, NP_ * i)]
     if typ == 1:
@@ -60,10 +58,9 @@ class Emu:
         return M[i * B:(i + 1) * B, j * B:(j + 1) * B]
 
     def run(self, t):
-        typ, part, i, j, k, whole = t
+        typ, part, i, j, k = t
         s = B // NP_  # strip width (32 of 128 on the device)
-        rows = slice(0, B) if whole else slice(part * s, (part + 1) * s)
-        inc = NP_ if whole else 1
+        rows = slice(part * s, (part + 1) * s)
         if typ == 0:  # LEAF(k = i): the leaf reads A_kk's lower triangle
             L = np.linalg.cholesky(np.tril(self.blk(self.A, i, i)) + np.tril(self.blk(self.A, i, i), -1).T)
             self.blk(self.X, i, i)[:] = np.linalg.inv(L)
@@ -73,23 +70,23 @@ class Emu:
         if typ == 1:  # TRSM(i, k): row strip of L_ik = A_ik X_kkᵀ (in place)
             C = self.blk(self.A, i, k)
             C[rows] = C[rows] @ self.blk(self.X, k, k).T
-            self.cnt["a"][i, k] += inc
+            self.cnt["a"][i, k] += 1
         elif typ == 2:  # UPD(i, j, k): row strip of A_ij −= L_ik L_jkᵀ (diagonal: lower blocks)
             C = self.blk(self.A, i, j)
             upd = self.blk(self.A, i, k)[rows] @ self.blk(self.A, j, k).T
             if i == j:  # waves right of the strip's diagonal block stay idle
                 upd[:, (part + 1) * s:] = 0.0
             C[rows] -= upd
-            self.cnt["a"][i, j] += inc
+            self.cnt["a"][i, j] += 1
         elif typ == 3:  # UPDX(i, k, j): row strip of S_ik (+)= L_ij X_jk (first term overwrites)
             C = self.blk(self.X, i, k)
             prod = self.blk(self.A, i, j)[rows] @ self.blk(self.X, j, k)
             C[rows] = prod if j == k else C[rows] + prod
-            self.cnt["x"][i, k] += inc
+            self.cnt["x"][i, k] += 1
         else:  # FIN(i, k): column strip of X_ik = −X_ii S_ik (in place)
             C = self.blk(self.X, i, k)
             C[:, rows] = -self.blk(self.X, i, i) @ C[:, rows]
-            self.cnt["x"][i, k] += inc
+            self.cnt["x"][i, k] += 1
 
 
 def spd(T, seed):
@@ -145,11 +142,9 @@ def test_queue_sizes():
     lib = _lib.load()
     for T in (2, 20, 40):
         n = lib.gps_dag_task_list(T, None, 0)
-        # TRSM and FIN: NP_ strips per tile; UPD on a diagonal tile and the first UPDX term
-        # (j == k): NP_ strips; the off-diagonal UPD / later UPDX terms: one whole-tile task each
-        strip_tiles = 4 * (T * (T - 1) // 2)
-        whole = 2 * (T * (T - 1) * (T - 2) // 6)
-        assert n == T + NP_ * strip_tiles + whole
+        upd = T * (T - 1) * (T + 1) // 6          # Σ_k (T−1−k)(T−k)/2
+        updx = (T - 1) * T * (T + 1) // 6         # Σ_j (T−1−j)(j+1)
+        assert n == T + NP_ * (T * (T - 1) + upd + updx)
     assert lib.gps_dag_task_list(65, None, 0) < 0 and lib.gps_dag_task_list(1, None, 0) < 0
 
 

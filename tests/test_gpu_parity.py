@@ -682,38 +682,6 @@ def test_persistent_factorisation_matches_recursion(gpu_ctx, n, tiles):
     assert abs(r1.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
-@pytest.mark.parametrize("n,tiles", [(5000, 40), (2561, 20)])
-def test_persistent_factorisation_whole_tile_tasks(gpu_ctx, n, tiles):
-    """GPS_OPT_DAG_WHOLE: the off-diagonal trailing updates as whole-tile tasks (one workgroup,
-    LDS-staged, the update accumulated onto the tile in place) or as 4 row strips: both against
-    the recursion down to the 128-leaf and the oracle (another summation order each)."""
-    import gpscore
-    from gpscore import _lib
-    rng = np.random.default_rng(n + 7)
-    d = 6
-    X = rng.standard_normal((n, d))
-    y = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n)
-    th = (0.2, np.log(1.7) * np.ones(d), np.log(0.02))
-    gp = gpscore.GP(ctx=gpu_ctx)
-    runs = {}
-    try:
-        for name, dag, whole in (("rec", False, 1), ("strips", True, 0), ("whole", True, 1)):
-            gpu_ctx.set_dag(dag, tiles)
-            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_WHOLE, whole)
-            runs[name] = gp.fit(X, y, th)
-    finally:
-        gpu_ctx.set_dag(True, 20)
-        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_WHOLE, 1)
-    f = O.fast_full_fit(X, y, *th)
-    for name in ("strips", "whole"):
-        r = runs[name]
-        assert nrel(r.mu_loo, runs["rec"].mu_loo) < 1e-11 and nrel(r.var_loo, runs["rec"].var_loo) < 1e-11
-        for k in ("nlml", "loo_crps", "loo_logs", "logdet", "quad"):
-            ref = runs["rec"].objectives[k]
-            assert abs(r.objectives[k] - ref) <= 1e-11 * max(1.0, abs(ref)), (name, k)
-        assert nrel(r.mu_loo, f["loo_mu"]) < 1e-9 and nrel(r.var_loo, f["loo_var"]) < 1e-9
-
-
 @pytest.mark.parametrize("n", [2560, 5000])
 def test_persistent_factorisation_load_groups_bitwise(gpu_ctx, n):
     """GPS_OPT_DAG_GROUP only changes how many operand chunks a strip task has in flight, not the

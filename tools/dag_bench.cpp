@@ -2,7 +2,7 @@
 // of T 128-tiles, standalone: timing over repeated launches, a sampled correctness check
 // (L·Lᵀ = A and L⁻¹·L = I on random entries), and one traced launch whose per-slot timestamps
 // go to a CSV for tools/dag_trace.py (critical path, hand-off latencies, per-type durations).
-//   dag_bench [T=20] [nwg=256] [trace.csv|-] [reps=20] [group=3] [order=1] [whole=1]
+//   dag_bench [T=20] [nwg=256] [trace.csv|-] [reps=20] [group=3] [order=1]
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -24,7 +24,6 @@ int main(int argc, char** argv) {
   const int reps = argc > 4 ? atoi(argv[4]) : 20;
   const int group = argc > 5 ? atoi(argv[5]) : 3;
   const int order = argc > 6 ? atoi(argv[6]) : 1;
-  const int whole = argc > 7 ? atoi(argv[7]) : 1;
   const int n = 128 * T, d = 8;
   // SPD test block: ARD-style Gram of random points + noise (what the recursion hands down)
   std::mt19937_64 rng(7);
@@ -37,7 +36,7 @@ int main(int argc, char** argv) {
       for (int k = 0; k < d; ++k) { const double t = X[i * d + k] - X[j * d + k]; s += t * t; }
       h[(size_t)i * n + j] = exp(-0.25 * s) + (i == j ? 0.05 : 0.0);
     }
-  const std::vector<uint32_t> tl = dag_task_list(T, order, whole != 0);
+  const std::vector<uint32_t> tl = dag_task_list(T, order);
   const int nt = (int)tl.size();
   double *A0, *A, *Li, *ld;
   int *info, *cnt;
