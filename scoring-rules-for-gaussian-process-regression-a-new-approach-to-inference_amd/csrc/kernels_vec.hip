@@ -90,6 +90,9 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const double* __restrict_
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= len) return;
   double s = init ? init[j] : 0.0;
+  // (8 slabs' loads in flight ahead of the in-order adds: the predictive pass sums 157 slabs,
+  // one memory latency each without the unroll)
+#pragma unroll 8
   for (int q = 0; q < nslab; ++q) s += slab[(int64_t)q * ld + j];
   out[j] = s;
 }
@@ -347,6 +350,7 @@ __global__ __launch_bounds__(256) void fitc_lambda_rows_kernel(
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n_pad) {
     double qi = 0.0;
+#pragma unroll 8
     for (int t = 0; t < nslab; ++t) qi += slab[(int64_t)t * ld + i];
     q[i] = qi;
     if (i < n) {
@@ -391,6 +395,7 @@ __global__ __launch_bounds__(256) void fitc_loo_rows_kernel(
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n_pad) {
     double ri = 0.0;
+#pragma unroll 8
     for (int t = 0; t < nslab; ++t) ri += slab[(int64_t)t * ld + i];
     r[i] = ri;
     if (i < n) {
