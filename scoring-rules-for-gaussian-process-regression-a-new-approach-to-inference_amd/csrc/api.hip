@@ -1562,16 +1562,20 @@ int full_fit_core(gps_ctx* ctx, int kind, const double* theta, int n_ell) {
     Prof pr(ctx, "gemv_beta", 0, 4.0 * (double)np * np);
     HIPCHK(launch_gemv_lower(ctx->Linv.d(), np, ctx->y.d(), ctx->beta.d(), (int)np, s));
   }
-  {
+  int nchunk_c = 0;
+  {  // α = L⁻ᵀβ and diag(A⁻¹) = colsum(L⁻¹∘L⁻¹): one column pass, chunk partials
     Prof pr(ctx, "colred_alpha_dinv", 0, 4.0 * (double)np * np);
-    HIPCHK(launch_colred(ctx->Linv.d(), np, (int)np, (int)np, 1, ctx->beta.d(), nullptr,
-                         ctx->alpha.d(), ctx->dinv.d(), ctx->slab.d(), s));
+    nchunk_c = launch_colred_partials(ctx->Linv.d(), np, (int)np, (int)np, 1, ctx->beta.d(),
+                                      ctx->slab.d(), s);
+    ARGCHK(nchunk_c > 0, "column pass launch failed");
   }
-  {
+  {  // chunk sums fused with the LOO rows (one thread per row, many workgroups)
+    double* part = row_part(ctx, np, 4);
+    ARGCHK(part != nullptr, "out of device memory");
     Prof pr(ctx, "loo_finalize", 0, 0);
-    HIPCHK(launch_full_loo(ctx->y.d(), ctx->alpha.d(), ctx->dinv.d(), ctx->beta.d(),
-                           ctx->logdiag.d(), (int)n, ctx->mu_loo.d(), ctx->var_loo.d(),
-                           ctx->small.d(), s));
+    HIPCHK(launch_full_loo(ctx->y.d(), ctx->slab.d(), nchunk_c, np, ctx->beta.d(),
+                           ctx->logdiag.d(), (int)n, ctx->alpha.d(), ctx->dinv.d(),
+                           ctx->mu_loo.d(), ctx->var_loo.d(), ctx->small.d(), part, s));
   }
   return 0;
 }

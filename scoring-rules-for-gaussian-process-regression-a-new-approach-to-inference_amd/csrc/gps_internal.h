@@ -231,9 +231,15 @@ hipError_t launch_sym_pack(const double* slab, int64_t slice_stride, int nslab, 
 hipError_t launch_sym_unpack(const double* packed, int m, int M, const double* base, int full,
                              double* dst, hipStream_t s);
 // full-GP LOO finalize (one workgroup): see kernels_vec.hip
-hipError_t launch_full_loo(const double* y, const double* alpha, const double* dinv,
-                           const double* beta, const double* logdiag, int n,
-                           double* mu_loo, double* var_loo, double* obj, hipStream_t s);
+// full-GP LOO: α, d = diag(A⁻¹) summed from the column pass's nslab chunk partials (slab:
+// [α chunks | d chunks], ld apart), stored, then μ/σ² LOO and obj = [nlml, loo_crps, loo_logs,
+// logdet, quad] (obj + 8: 4 scratch sums; part: ⌈n_pad/256⌉·4 doubles)
+hipError_t launch_full_loo(const double* y, const double* slab, int nslab, int64_t ld,
+                           const double* beta, const double* logdiag, int n, double* alpha,
+                           double* dinv, double* mu_loo, double* var_loo, double* obj,
+                           double* part, hipStream_t s);
+int launch_colred_partials(const double* M, int64_t ldm, int rows, int cols, int lower,
+                           const double* w, double* slab, hipStream_t s);
 // predictive variance finalize + test-score partial sums
 hipError_t launch_pred_finalize(const double* s1, const double* s2, int nt, double base_var,
                                 double* mu, double* var, hipStream_t s);

@@ -121,6 +121,17 @@ hipError_t launch_colred(const double* M, int64_t ldm, int rows, int cols, int l
   return hipSuccess;
 }
 
+// the column pass alone: chunk partials of Σ w_r M_rc (slab) and Σ M_rc² (slab + nchunk·cols);
+// returns the chunk count (the caller sums the chunks, e.g. fused into its row finaliser)
+int launch_colred_partials(const double* M, int64_t ldm, int rows, int cols, int lower,
+                           const double* w, double* slab, hipStream_t s) {
+  if ((cols & 1) || (ldm & 1)) return -1;
+  const int nchunk = (rows + CR_ROWS - 1) / CR_ROWS;
+  hipLaunchKernelGGL(colred_kernel, dim3((cols + CR_COLS - 1) / CR_COLS, nchunk), dim3(256), 0, s,
+                     M, ldm, rows, cols, lower, w, nullptr, slab, slab + (int64_t)nchunk * cols);
+  return hipGetLastError() == hipSuccess ? nchunk : -1;
+}
+
 // sum split-K slabs of a symmetric M×M accumulator; tile-lower kept, strict-upper
 // tiles zeroed (so the buffer can be all-reduced / factorised as is)
 __global__ __launch_bounds__(256) void sym_slab_sum_kernel(const double* __restrict__ slab,
@@ -203,51 +214,6 @@ hipError_t launch_sym_unpack(const double* packed, int m, int M, const double* b
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------ full-GP LOO
-// obj: [nlml, loo_crps, loo_logs, logdet, quad]; logdiag/beta over n_pad (pad = 0)
-__global__ __launch_bounds__(1024) void full_loo_kernel(const double* __restrict__ y,
-                                                        const double* __restrict__ alpha,
-                                                        const double* __restrict__ dinv,
-                                                        const double* __restrict__ beta,
-                                                        const double* __restrict__ logdiag, int n,
-                                                        int n_pad, double* __restrict__ mu_loo,
-                                                        double* __restrict__ var_loo,
-                                                        double* __restrict__ obj) {
-  __shared__ double sh[4 * 16];
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int i = threadIdx.x; i < n_pad; i += blockDim.x) {
-    v[2] += logdiag[i];
-    v[3] = fma(beta[i], beta[i], v[3]);
-    if (i < n) {
-      const double d = dinv[i];
-      const double m = y[i] - alpha[i] / d;
-      const double c = 1.0 / d;
-      mu_loo[i] = m;
-      var_loo[i] = c;
-      v[0] += crps_term(m, c, y[i]);
-      v[1] += logs_term(m, c, y[i]);
-    }
-  }
-  block_sum<4>(v, sh);
-  if (threadIdx.x == 0) {
-    const double logdet = 2.0 * v[2], quad = v[3];
-    obj[0] = 0.5 * n * 1.83787706640934548356 + 0.5 * logdet + 0.5 * quad;
-    obj[1] = v[0] / n;
-    obj[2] = v[1] / n;
-    obj[3] = logdet;
-    obj[4] = quad;
-  }
-}
-
-hipError_t launch_full_loo(const double* y, const double* alpha, const double* dinv,
-                           const double* beta, const double* logdiag, int n, double* mu_loo,
-                           double* var_loo, double* obj, hipStream_t s) {
-  const int n_pad = (int)pad_to(n);
-  hipLaunchKernelGGL(full_loo_kernel, dim3(1), dim3(1024), 0, s, y, alpha, dinv, beta, logdiag, n,
-                     n_pad, mu_loo, var_loo, obj);
-  return hipGetLastError();
-}
-
 // ------------------------------------------------------ two-level row sums
 // The row finalisers below run one thread per row over many workgroups (a single workgroup
 // walking 40k-200k rows took 30-105 µs of a FITC unit's critical path); each workgroup writes
@@ -267,6 +233,67 @@ __global__ __launch_bounds__(1024) void partials_sum_kernel(const double* __rest
   if (threadIdx.x == 0)
 #pragma unroll
     for (int q = 0; q < NV; ++q) out[q] = v[q];
+}
+
+// ------------------------------------------------------------ full-GP LOO
+// α_i = Σ_t slab1[t][i] and d_i = Σ_t slab2[t][i] (the column pass's chunk partials, summed in
+// chunk order as slab_sum_kernel does), stored, then the LOO closed form (R&W 5.12, KF:241-244)
+// per row; per-workgroup partials [Σ crps, Σ logs, Σ log L_ii, Σ β²] (pads carry zeros)
+__global__ __launch_bounds__(256) void full_loo_rows_kernel(
+    const double* __restrict__ y, const double* __restrict__ slab1, const double* __restrict__ slab2,
+    int64_t ld, int nslab, const double* __restrict__ beta, const double* __restrict__ logdiag,
+    int n, int n_pad, double* __restrict__ alpha, double* __restrict__ dinv,
+    double* __restrict__ mu_loo, double* __restrict__ var_loo, double* __restrict__ part) {
+  __shared__ double sh[4 * 16];
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n_pad) {
+    double a = 0.0, dd = 0.0;
+#pragma unroll 8
+    for (int t = 0; t < nslab; ++t) {
+      a += slab1[(int64_t)t * ld + i];
+      dd += slab2[(int64_t)t * ld + i];
+    }
+    alpha[i] = a;
+    dinv[i] = dd;
+    v[2] = logdiag[i];
+    v[3] = beta[i] * beta[i];
+    if (i < n) {
+      const double m = y[i] - a / dd;
+      const double c = 1.0 / dd;
+      mu_loo[i] = m;
+      var_loo[i] = c;
+      v[0] = crps_term(m, c, y[i]);
+      v[1] = logs_term(m, c, y[i]);
+    }
+  }
+  block_sum<4>(v, sh);
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 4; ++q) part[(int64_t)blockIdx.x * 4 + q] = v[q];
+}
+// obj: [nlml, loo_crps, loo_logs, logdet, quad] from the sums [Σcrps, Σlogs, Σlog L_ii, Σβ²]
+__global__ void full_loo_obj_kernel(const double* __restrict__ sums, int n, double* __restrict__ obj) {
+  if (threadIdx.x != 0) return;
+  const double logdet = 2.0 * sums[2], quad = sums[3];
+  obj[0] = 0.5 * n * 1.83787706640934548356 + 0.5 * logdet + 0.5 * quad;
+  obj[1] = sums[0] / n;
+  obj[2] = sums[1] / n;
+  obj[3] = logdet;
+  obj[4] = quad;
+}
+
+hipError_t launch_full_loo(const double* y, const double* slab, int nslab, int64_t ld,
+                           const double* beta, const double* logdiag, int n, double* alpha,
+                           double* dinv, double* mu_loo, double* var_loo, double* obj,
+                           double* part, hipStream_t s) {
+  const int n_pad = (int)pad_to(n);
+  const int nblk = n_pad / 256 + (n_pad % 256 ? 1 : 0);
+  hipLaunchKernelGGL(full_loo_rows_kernel, dim3(nblk), dim3(256), 0, s, y, slab,
+                     slab + (int64_t)nslab * ld, ld, nslab, beta, logdiag, n, n_pad, alpha, dinv,
+                     mu_loo, var_loo, part);
+  hipLaunchKernelGGL(partials_sum_kernel<4>, dim3(1), dim3(1024), 0, s, part, nblk, obj + 8);
+  hipLaunchKernelGGL(full_loo_obj_kernel, dim3(1), dim3(64), 0, s, obj + 8, n, obj);
+  return hipGetLastError();
 }
 
 // --------------------------------------------------------------- predictive
