@@ -236,14 +236,16 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
 
 /* ---- objective surfaces (contour-plot.R) ---------------
  * The objectives of CP.R:43-85 on a length-scale × noise grid, one small full GP per grid
- * point (n <= 128; CP.R uses n = 20 points and a 50 × 50 grid, CP.R:88-141): kernel
+ * point (CP.R uses n = 20 points and a 50 × 50 grid, CP.R:88-141): kernel
  * sf²·exp(−½‖x − x'‖²/ℓ²) with ℓ = ell[j] (CP.R:15-23, not a log) and noise s.d. s = noise_sd[i]
  * entering as s² (CP.R:45).  out (4 · n_noise · n_ell, row-major [objective][i][j], R's
  * matrix(…, nrow = 50) orientation): GPS_SURF_LOO_CRPS (cal_m_crps CP.R:43-53),
  * GPS_SURF_INSAMPLE_CRPS (wrong_cal_m_crps CP.R:55-64), GPS_SURF_NLML (cal_NLML CP.R:68-73),
  * GPS_SURF_LOO_LOGS (cal_m_logs CP.R:75-85).  flags GPS_SURF_LOGS_ADD_NOISE: the LOO-LogS
  * variance is 1/d + s² as CP.R:81 writes it; without it 1/d (the KF:416-424 form).  A grid
- * point whose matrix is not positive definite gets NaN objectives. */
+ * point whose matrix is not positive definite gets NaN objectives.  n > 128: each grid point
+ * is one resident fit (the gps_full_fit path) and X, y become the context's full-GP data, as
+ * after gps_full_set_data (no fit is left in place). */
 enum { GPS_SURF_LOO_CRPS = 0, GPS_SURF_INSAMPLE_CRPS = 1, GPS_SURF_NLML = 2, GPS_SURF_LOO_LOGS = 3,
        GPS_N_SURF = 4 };
 enum { GPS_SURF_LOGS_ADD_NOISE = 1 };

@@ -2822,11 +2822,47 @@ int gps_full_surface(gps_ctx* ctx, const double* X, const double* y, int64_t n, 
                      int64_t n_noise, int flags, double* out) {
   if (int rc = bind(ctx)) return rc;
   ARGCHK(X && y && ell && noise_sd && out, "NULL argument");
-  ARGCHK(n >= 1 && n <= GPS_SURFACE_MAX_N, "surface: n must be in 1..128 (one wavefront per point)");
+  ARGCHK(n >= 1, "surface: n must be >= 1");
   ARGCHK(d >= 1 && d <= GPS_MAX_D, "bad d");
   ARGCHK(n_ell >= 1 && n_noise >= 1 && n_ell * n_noise <= (1 << 24), "bad grid");
   ARGCHK((flags & ~GPS_SURF_LOGS_ADD_NOISE) == 0, "unknown surface flag");
   hipStream_t s = ctx->stream;
+  if (n > GPS_SURFACE_MAX_N) {
+    // beyond one wavefront's LDS: one resident fit per grid point (the gps_full_fit path:
+    // Gram, factorisation, β, α, diag(A⁻¹), LOO sums), then the in-sample CRPS and the CP.R:81
+    // LogS from α and diag(A⁻¹); the data become the context's resident full-GP data
+    ARGCHK(n > 1, "surface: n must be > 1");
+    if (int rc = gps_full_set_data(ctx, X, y, n, d)) return rc;
+    const int64_t st = n_noise * n_ell;
+    for (int64_t i = 0; i < n_noise; ++i)
+      for (int64_t j = 0; j < n_ell; ++j) {
+        const double s2 = noise_sd[i] * noise_sd[i];
+        const double theta[3] = {log_sf2, std::log(std::fabs(ell[j])), std::log(s2)};  // ℓ² enters
+        const int64_t g = i * n_ell + j;
+        int rc = full_fit_core(ctx, GPS_ARD, theta, 1);
+        double* part = rc == 0 ? row_part(ctx, n, 2) : nullptr;
+        if (rc == 0) {
+          ARGCHK(part != nullptr, "out of device memory");
+          HIPCHK(launch_surface_point_sums(ctx->y.d(), ctx->alpha.d(), ctx->dinv.d(), (int)n, s2,
+                                           (flags & GPS_SURF_LOGS_ADD_NOISE) ? 1 : 0,
+                                           ctx->small.d() + 16, part, s));
+          HIPCHK(hipMemcpyAsync(ctx->hsmall, ctx->small.p, 18 * 8, hipMemcpyDeviceToHost, s));
+          rc = check_info(ctx);
+        }
+        if (rc > 0) {  // not positive definite at this point: NaN there only (as the kernel)
+          for (int q = 0; q < 4; ++q) out[q * st + g] = std::nan("");
+          continue;
+        }
+        if (rc < 0) return rc;
+        const double* h = ctx->hsmall;
+        out[g] = h[GPS_OBJ_LOO_CRPS];
+        out[st + g] = h[16] / (double)n;
+        out[2 * st + g] = h[GPS_OBJ_NLML];
+        out[3 * st + g] = h[17] / (double)n;
+      }
+    ctx->fitted = false;  // the last point's factor is not a fit the caller asked for
+    return 0;
+  }
   if (int rc = upload(ctx, ctx->t0, X, n, d, n)) return rc;
   if (int rc = upload(ctx, ctx->t1, y, n, 1, n)) return rc;
   if (int rc = upload(ctx, ctx->t2, ell, n_ell, 1, n_ell)) return rc;

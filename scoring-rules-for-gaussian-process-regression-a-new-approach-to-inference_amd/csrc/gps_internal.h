@@ -238,6 +238,10 @@ hipError_t launch_full_loo(const double* y, const double* slab, int nslab, int64
                            const double* beta, const double* logdiag, int n, double* alpha,
                            double* dinv, double* mu_loo, double* var_loo, double* obj,
                            double* part, hipStream_t s);
+// CP.R surface point from a resident fit: sums [Σ in-sample CRPS, Σ LOO-LogS (+ s² if add_noise)]
+hipError_t launch_surface_point_sums(const double* y, const double* alpha, const double* dinv,
+                                     int n, double s2, int add_noise, double* sums, double* part,
+                                     hipStream_t s);
 int launch_colred_partials(const double* M, int64_t ldm, int rows, int cols, int lower,
                            const double* w, double* slab, hipStream_t s);
 // predictive variance finalize + test-score partial sums

@@ -296,6 +296,37 @@ hipError_t launch_full_loo(const double* y, const double* slab, int nslab, int64
   return hipGetLastError();
 }
 
+// CP.R surface point from a resident fit (n > GPS_SURFACE_MAX_N): the "wrong" in-sample CRPS
+// (CP.R:55-64: μ = y − s²α, c = 2s² − s⁴ d) and the LOO-LogS with CP.R:81's + s² (or not),
+// from α and d = diag(A⁻¹) — the surface kernel's formulas (kernels_surface.hip)
+__global__ __launch_bounds__(256) void surface_point_rows_kernel(
+    const double* __restrict__ y, const double* __restrict__ alpha, const double* __restrict__ dinv,
+    int n, double s2, int add_noise, double* __restrict__ part) {
+  __shared__ double sh[2 * 16];
+  double v[2] = {0.0, 0.0};
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const double a = alpha[i], dj = dinv[i], yi = y[i];
+    const double mu = yi - a / dj, c = 1.0 / dj;
+    v[0] = crps_term(yi - s2 * a, 2.0 * s2 - s2 * s2 * dj, yi);
+    v[1] = logs_term(mu, add_noise ? c + s2 : c, yi);
+  }
+  block_sum<2>(v, sh);
+  if (threadIdx.x == 0) {
+    part[(int64_t)blockIdx.x * 2] = v[0];
+    part[(int64_t)blockIdx.x * 2 + 1] = v[1];
+  }
+}
+hipError_t launch_surface_point_sums(const double* y, const double* alpha, const double* dinv,
+                                     int n, double s2, int add_noise, double* sums, double* part,
+                                     hipStream_t s) {
+  const int nblk = std::max(1, (n + 255) / 256);
+  hipLaunchKernelGGL(surface_point_rows_kernel, dim3(nblk), dim3(256), 0, s, y, alpha, dinv, n, s2,
+                     add_noise, part);
+  hipLaunchKernelGGL(partials_sum_kernel<2>, dim3(1), dim3(1024), 0, s, part, nblk, sums);
+  return hipGetLastError();
+}
+
 // --------------------------------------------------------------- predictive
 __global__ __launch_bounds__(256) void pred_finalize_kernel(const double* __restrict__ s1,
                                                             const double* __restrict__ s2, int nt,

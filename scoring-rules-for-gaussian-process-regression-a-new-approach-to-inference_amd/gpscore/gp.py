@@ -337,7 +337,8 @@ def fit(X, y, theta, kind="full", Z=None, rbf=False, ctx=None):
 
 def surface(X, y, ell_grid, noise_sd_grid, log_sf2=0.0, logs_add_noise=True, ctx=None):
     """The objective surfaces of contour-plot.R (CP.R:43-85) over a length-scale × noise grid,
-    one small full GP per grid point on the device (n <= 128).
+    one small full GP per grid point on the device (n <= 128: one wavefront each; beyond that
+    one resident fit per point, and X, y become the context's full-GP data).
 
     ``ell_grid`` holds length-scales ℓ (not logs; CP.R's ``l``), ``noise_sd_grid`` noise
     standard deviations s entering as s² (CP.R's ``j``); the kernel is

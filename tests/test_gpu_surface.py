@@ -56,7 +56,7 @@ def test_surface_matches_single_point_fits(gpu_ctx):
 
 def test_surface_edge_cases(gpu_ctx):
     """n = 1, n = 128 (the LDS limit), a non-PD grid point (duplicate inputs, s = 0) → NaN
-    there only, and n > 128 rejected."""
+    there only."""
     import gpscore
     import gp_oracle as O
     x1, y1 = np.array([[0.3]]), np.array([0.7])
@@ -74,8 +74,34 @@ def test_surface_edge_cases(gpu_ctx):
     xd = np.array([[0.0], [0.0], [1.0]])
     s = gpscore.surface(xd, np.array([1.0, 1.0, 0.0]), [1.0], [0.0, 0.1], ctx=gpu_ctx)
     assert np.all(np.isnan(s["nlml"][0])) and np.all(np.isfinite(s["nlml"][1]))
-    with pytest.raises(gpscore.GpsError):
-        gpscore.surface(np.zeros((129, 1)), np.zeros(129), [1.0], [0.1], ctx=gpu_ctx)
+
+
+@pytest.mark.parametrize("n", [129, 700])
+def test_surface_beyond_one_wavefront(gpu_ctx, n):
+    """n > 128 (past one wavefront's LDS): each grid point runs the resident full-GP path
+    (gps_full_fit's factorisation and LOO sums, the in-sample CRPS and CP.R:81's LogS from α and
+    diag(A⁻¹)); against the oracle's CP.R objectives, a non-PD point (s = 0 with duplicate
+    inputs) NaN there only, and the data left as the context's resident full-GP data."""
+    import gpscore
+    import gp_oracle as O
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-4, 4, (n, 2))
+    y = np.cos(x.sum(1)) + 0.1 * rng.standard_normal(n)
+    ell, sd = [0.6, 1.4, 2.5], [0.05, 0.3]
+    s = gpscore.surface(x, y, ell, sd, ctx=gpu_ctx)
+    for flag in (True, False):
+        s = gpscore.surface(x, y, ell, sd, logs_add_noise=flag, ctx=gpu_ctx)
+        ref = O.cp_surface(x, y, ell, sd, logs_add_noise=flag)
+        for k, nm in enumerate(NAMES):
+            assert nrel(s[nm], ref[k]) < 1e-9, (nm, flag, nrel(s[nm], ref[k]))
+    # rows 0 and 1 identical: with s = 0 the second pivot is exactly 1 − 1·1 = 0 (not PD)
+    xd = np.vstack([x[:1], x[:1], x[2:]])
+    s = gpscore.surface(xd, y, [1.0], [0.0, 0.1], ctx=gpu_ctx)
+    assert np.all(np.isnan(s["nlml"][0])) and np.all(np.isfinite(s["nlml"][1]))
+    gp = gpscore.GP(ctx=gpu_ctx)  # the surface's data are the resident full-GP data now
+    r = gp.fit(theta=(0.0, np.log(1.0), np.log(0.01)))
+    f = O.fast_full_fit(xd, y, 0.0, np.log(1.0), np.log(0.01))
+    assert abs(r.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
 def test_surface_concurrent_contexts():
