@@ -104,6 +104,7 @@ struct gps_ctx {
   bool dag = true;                     // GPS_OPT_DAG: persistent factorisation of the bottom blocks
   int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
+  int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: one per CU)
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
@@ -441,7 +442,8 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
-    HIPCHK(launch_potrf_dag(d, std::min(ctx->ncu, std::max(4, 2 * nb * nb)), s));
+    const int nwg = std::min(ctx->dag_wgs > 0 ? ctx->dag_wgs : ctx->ncu, std::max(4, 2 * nb * nb));
+    HIPCHK(launch_potrf_dag(d, nwg, s));
     return 0;
   }
   const int n1b = nb / 2, n2b = nb - n1b;
@@ -593,7 +595,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
-      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_cnt.p};
+      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_cnt.p};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
@@ -1239,6 +1241,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
     case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;
     case GPS_OPT_DAG: ctx->dag = value != 0; return 0;
+    case GPS_OPT_DAG_WGS:
+      ARGCHK(value >= 0, "GPS_OPT_DAG_WGS must be >= 0");
+      ctx->dag_wgs = value;
+      return 0;
     case GPS_OPT_DAG_GROUP:
       ARGCHK(value >= 2 && value <= 4, "GPS_OPT_DAG_GROUP must be 2, 3 or 4");
       ctx->dag_group = value;

@@ -682,6 +682,29 @@ def test_persistent_factorisation_matches_recursion(gpu_ctx, n, tiles):
     assert abs(r1.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
+def test_persistent_factorisation_any_grid_bitwise(gpu_ctx):
+    """GPS_OPT_DAG_WGS: the queue is a topological order and every task's arithmetic is fixed, so
+    4 workgroups (a near-serial drain) and one per CU give the same bits."""
+    import gpscore
+    from gpscore import _lib
+    rng = np.random.default_rng(11)
+    n, d = 2560, 5
+    X = rng.standard_normal((n, d))
+    y = np.cos(X.sum(1)) + 0.1 * rng.standard_normal(n)
+    th = (0.1, np.log(1.5) * np.ones(d), np.log(0.03))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    runs = []
+    try:
+        for w in (0, 4, 96):
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_WGS, w)
+            runs.append(gp.fit(X, y, th))
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_WGS, 0)
+    for r in runs[1:]:
+        assert r.objectives == runs[0].objectives
+        assert np.array_equal(r.mu_loo, runs[0].mu_loo) and np.array_equal(r.var_loo, runs[0].var_loo)
+
+
 @pytest.mark.parametrize("n", [2560, 5000])
 def test_persistent_factorisation_load_groups_bitwise(gpu_ctx, n):
     """GPS_OPT_DAG_GROUP only changes how many operand chunks a strip task has in flight, not the
