@@ -1974,7 +1974,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   const int64_t red_len = mp * mp + mp + 8;
   HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
   const int64_t nchunk = (std::max(np, mp) + 255) / 256;
-  const int64_t fslab_len = std::max<int64_t>(tm * np, nchunk * mp * 2);
+  // (row-norm partials tm·np; column passes' chunk partials: Knm's 256-row chunks, and the
+  //  m×m pass for c in 32-row chunks)
+  const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * np, nchunk * mp * 2),
+                                              (mp + 31) / 32 * mp);
   HIPCHK(ensure(ctx->fslab, (size_t)fslab_len * 8));
   double* red = ctx->red.d();
   double* Bacc = red;
@@ -2038,8 +2041,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   {  // c = Lb⁻ᵀ Lb⁻¹ b
     Prof pr(ctx, "fitc_c", 0, 0);
     HIPCHK(launch_gemv_lower(ctx->Lb.d(), mp, bvec, ctx->tvec.d(), (int)mp, s));
+    // (32-row chunks: an m×m pass has few 256-row chunks, 32 workgroups at m = 2048; fslab
+    //  holds the m/32 chunk partials)
     HIPCHK(launch_colred(ctx->Lb.d(), mp, (int)mp, (int)mp, 1, ctx->tvec.d(), nullptr, ctx->c.d(),
-                         nullptr, ctx->fslab.d(), s));
+                         nullptr, ctx->fslab.d(), s, 32));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
   {  // r_i = ‖Lb⁻¹ k_i‖², and g = Knm c from the same pass over Knm (its last column tile)

@@ -215,7 +215,7 @@ hipError_t launch_gemv_full(const double* M, int64_t ldm, const double* x, doubl
 // Uses slab (>= nchunks*cols*2 doubles) and reduces into s1/s2.
 hipError_t launch_colred(const double* M, int64_t ldm, int rows, int cols, int lower,
                          const double* w, const double* rowscale, double* s1, double* s2,
-                         double* slab, hipStream_t s);
+                         double* slab, hipStream_t s, int crows = 256);
 // out[j] = sum_{s < nslab} slab[s*ld + j] (+ init[j] if init), j < len
 hipError_t launch_slab_sum(const double* slab, int64_t ld, int nslab, int64_t len,
                            const double* init, double* out, hipStream_t s);

@@ -49,7 +49,7 @@ constexpr int CR_ROWS = 256;  // rows per chunk
 constexpr int CR_COLS = 512;  // columns per block (2 per thread)
 
 __global__ __launch_bounds__(256) void colred_kernel(const double* __restrict__ M, int64_t ldm,
-                                                     int rows, int cols, int lower,
+                                                     int rows, int cols, int lower, int crows,
                                                      const double* __restrict__ w,
                                                      const double* __restrict__ rowscale,
                                                      double* __restrict__ slab1,
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void colred_kernel(const double* __restrict__ 
   const int c = blockIdx.x * CR_COLS + 2 * threadIdx.x;
   const int chunk = blockIdx.y;
   if (c >= cols) return;
-  int r0 = chunk * CR_ROWS, r1 = min(rows, r0 + CR_ROWS);
+  int r0 = chunk * crows, r1 = min(rows, r0 + crows);
   if (lower) r0 = max(r0, (c / GPS_TILE) * GPS_TILE);
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
   // (unrolled so 8 rows' loads are in flight ahead of the in-order FMAs: one memory latency
@@ -107,13 +107,13 @@ hipError_t launch_slab_sum(const double* slab, int64_t ld, int nslab, int64_t le
 
 hipError_t launch_colred(const double* M, int64_t ldm, int rows, int cols, int lower,
                          const double* w, const double* rowscale, double* s1, double* s2,
-                         double* slab, hipStream_t s) {
-  if ((cols & 1) || (ldm & 1)) return hipErrorInvalidValue;
-  const int nchunk = (rows + CR_ROWS - 1) / CR_ROWS;  // (CR_ROWS rows per chunk: see the kernel)
+                         double* slab, hipStream_t s, int crows) {
+  if ((cols & 1) || (ldm & 1) || crows < 1) return hipErrorInvalidValue;
+  const int nchunk = (rows + crows - 1) / crows;
   double* slab1 = s1 ? slab : nullptr;
   double* slab2 = s2 ? slab + (int64_t)nchunk * cols : nullptr;
   hipLaunchKernelGGL(colred_kernel, dim3((cols + CR_COLS - 1) / CR_COLS, nchunk), dim3(256), 0, s,
-                     M, ldm, rows, cols, lower, w, rowscale, slab1, slab2);
+                     M, ldm, rows, cols, lower, crows, w, rowscale, slab1, slab2);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (s1 && (e = launch_slab_sum(slab1, cols, nchunk, cols, nullptr, s1, s)) != hipSuccess) return e;
@@ -128,7 +128,7 @@ int launch_colred_partials(const double* M, int64_t ldm, int rows, int cols, int
   if ((cols & 1) || (ldm & 1)) return -1;
   const int nchunk = (rows + CR_ROWS - 1) / CR_ROWS;
   hipLaunchKernelGGL(colred_kernel, dim3((cols + CR_COLS - 1) / CR_COLS, nchunk), dim3(256), 0, s,
-                     M, ldm, rows, cols, lower, w, nullptr, slab, slab + (int64_t)nchunk * cols);
+                     M, ldm, rows, cols, lower, CR_ROWS, w, nullptr, slab, slab + (int64_t)nchunk * cols);
   return hipGetLastError() == hipSuccess ? nchunk : -1;
 }
 
