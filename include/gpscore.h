@@ -106,8 +106,9 @@ enum {
                              most 3/4 full splits that round's tiles into equal K runs over every
                              slot (in-launch fixed-order combine); 0: one workgroup per tile.
                              Process-wide. */
-  GPS_OPT_DAG_WGS = 19,   /* workgroups of a persistent factorisation launch (0, the default: one
-                             per CU); fewer leave CUs to a concurrent side-stream product */
+  GPS_OPT_DAG_WGS = 19,   /* workgroups of a persistent factorisation launch; 0 (default):
+                             automatic — one per CU for the full GP, half the CUs for the FITC
+                             m×m factorisations (the test pre-pass runs beside them) */
   GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
                              flight per load group (2, 3 (default) or 4).  Same values bitwise. */
 };

@@ -104,7 +104,8 @@ struct gps_ctx {
   bool dag = true;                     // GPS_OPT_DAG: persistent factorisation of the bottom blocks
   int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
-  int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: one per CU)
+  int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: automatic, see dag_width)
+  bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
@@ -442,7 +443,12 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
-    const int nwg = std::min(ctx->dag_wgs > 0 ? ctx->dag_wgs : ctx->ncu, std::max(4, 2 * nb * nb));
+    // width: one workgroup per CU, or half the CUs for the FITC m×m factorisations, whose chain
+    // needs ~70 workgroups at m = 2048 and whose side stream (the test pre-pass) then gets the
+    // other half (C4 12.72 -> 12.29 ms; the full GP's blocks want every CU: 124.2 vs 126.1 ms,
+    // profiles/r3_dag_width_ab.txt)
+    const int auto_w = ctx->dag_half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
+    const int nwg = std::min(ctx->dag_wgs > 0 ? ctx->dag_wgs : auto_w, std::max(4, 2 * nb * nb));
     HIPCHK(launch_potrf_dag(d, nwg, s));
     return 0;
   }
@@ -595,7 +601,8 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
-      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_cnt.p};
+      (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_half,
+      (uintptr_t)ctx->dag_cnt.p};
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
@@ -2002,7 +2009,9 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lm.d();
+  ctx->dag_half = true;  // (the FITC m×m factorisations: see potrf_inv_rec's width)
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr);
+  ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
   if (rc) return rc;
   HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
@@ -2035,8 +2044,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
   else
     HIPCHK(launch_sym_slab_sum(Bacc, 0, 1, (int)mp, ctx->Kmm.d(), ctx->Am.d(), s));
-  if ((rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr)))
-    return rc;
+  ctx->dag_half = true;
+  rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr);
+  ctx->dag_half = false;
+  if (rc) return rc;
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
   {  // c = Lb⁻ᵀ Lb⁻¹ b
     Prof pr(ctx, "fitc_c", 0, 0);
