@@ -164,6 +164,7 @@ struct gps_ctx {
   // test-side ‖Lm⁻¹k_*‖² formed by gps_fitc_fit on aux[0] during Lb's factorisation
   bool f_pre = false;
   hipEvent_t pre_fork = nullptr, pre_join = nullptr;
+  hipEvent_t kn_fork = nullptr, kn_join = nullptr;  // the FITC Knm Gram beside Lm's factorisation
   DBuf fslab_pre;
   Theta fth;
   // ---- comm: RCCL (gps_comm_init) or the in-process group (gps_comm_init_local)
@@ -1190,7 +1191,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join})
+  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->kn_fork, ctx->kn_join})
     if (e) (void)hipEventDestroy(e);
   for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1998,13 +1999,23 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                  ctx->Kmm.d(), mp, (int)mp, (int)mp)))
     return rc;
   HIPCHK(hipMemcpyAsync(ctx->Am.p, ctx->Kmm.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
-  // this shard's rows of K(X, Z) first: the q column tiles [0, n1) run on aux[0] during Lm's
-  // factorisation (PRE_FITC_Q) as soon as the top-level Lm11⁻¹ is final
-  if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
-                 ctx->Knm.d(), mp, (int)np, (int)mp)))
-    return rc;
   // (a persistent top level has no recursion step to overlap the pre-pass with)
   const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
+  // this shard's rows of K(X, Z): with a pre-pass, first on the main stream (the q column tiles
+  // [0, n1) then run on aux[0] inside Lm's captured factorisation, as soon as the top-level
+  // Lm11⁻¹ is final); without one, on aux[0] beside Lm's factorisation, whose persistent blocks
+  // leave half the CUs free (it needs only X, Z), joined before the q pass
+  const bool kside = !preq && ctx->overlap && !ctx->prof;
+  if (kside) {  // (dedicated events: the factorisation reuses its pool of sync events)
+    for (hipEvent_t* e : {&ctx->kn_fork, &ctx->kn_join})
+      if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->kn_fork, s));
+    HIPCHK(hipStreamWaitEvent(ctx->aux[0], ctx->kn_fork, 0));
+  }
+  if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
+                 ctx->Knm.d(), mp, (int)np, (int)mp, kside ? ctx->aux[0] : nullptr)))
+    return rc;
+  if (kside) HIPCHK(hipEventRecord(ctx->kn_join, ctx->aux[0]));
   const int64_t qn1 = preq ? (mp / GPS_TILE / 2) * GPS_TILE : 0;
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
@@ -2013,6 +2024,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr);
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
+  if (kside) HIPCHK(hipStreamWaitEvent(s, ctx->kn_join, 0));  // (before any return: Knm in flight)
   if (rc) return rc;
   HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
   // q_i = ‖Lm⁻¹ k_i‖² (the remaining column tiles)
