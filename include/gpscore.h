@@ -106,8 +106,6 @@ enum {
                              most 3/4 full splits that round's tiles into equal K runs over every
                              slot (in-launch fixed-order combine); 0: one workgroup per tile.
                              Process-wide. */
-  GPS_OPT_GEMM_WAVES = 20, /* 4 (default) or 8 waves per 128-tile workgroup of the plain-store
-                              GEMM (8: 64×32 per wave, four waves per SIMD).  Process-wide. */
   GPS_OPT_DAG_WGS = 19,   /* workgroups of a persistent factorisation launch; 0 (default):
                              automatic — one per CU for the full GP, half the CUs for the FITC
                              m×m factorisations (the test pre-pass runs beside them) */

@@ -125,7 +125,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <int ALAY, int BLAY, int EPI, int TILE, int NW = 4>
+template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o = -1, int ke_o = -1,
                                           double* part = nullptr);
@@ -151,27 +151,13 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, blockIdx.y, smem);
 }
 
-// The same 128-tile with 8 waves of 64×32 (GPS_OPT_GEMM_WAVES = 8, A/B): half the accumulators
-// per wave, so two workgroups per CU put four waves on each SIMD instead of two — more waves to
-// issue MFMAs while the others wait at their workgroup's barrier.  EPI_STORE only.
-template <int ALAY, int BLAY>
-__global__ __launch_bounds__(512) void gemm_f64_kernel8(GemmParams p) {
-  constexpr int LS = 128 + 16;
-  constexpr int STAGE = 2 * BK * LS;
-  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
-  const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
-  int ti, tj;
-  if (!tile_of(p, remap ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x, ti, tj)) return;
-  gemm_tile<ALAY, BLAY, EPI_STORE, 128, 8>(p, ti, tj, blockIdx.y, smem);
-}
-
 // EPI_STORE epilogue: C = alpha·acc (+ beta·C) for this thread's accumulators
-template <int TILE, int NW = 4>
+template <int TILE>
 __device__ __forceinline__ void store_acc(const GemmParams& p, int ti, int tj, int kslice,
-                                          const d4 (&acc)[TILE / 32][TILE * 2 / NW / 16]) {
-  constexpr int WT = TILE / 2, WTN = TILE * 2 / NW, MI = WT / 16, NI = WTN / 16;
+                                          const d4 (&acc)[TILE / 32][TILE / 32]) {
+  constexpr int WT = TILE / 2, MI = WT / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / (NW / 2), wc = wave % (NW / 2);
+  const int wr = wave >> 1, wc = wave & 1;
   const int lrow = lane >> 4, lcol = lane & 15;
   const int row0 = ti * TILE, col0 = tj * TILE;
   double* Cb = p.C + (int64_t)kslice * p.c_kslice_stride;
@@ -180,9 +166,9 @@ __device__ __forceinline__ void store_acc(const GemmParams& p, int ti, int tj, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = row0 + wr * WT + mi * 16 + lrow + 4 * r;
-      double* crow = Cb + (int64_t)row * p.ldc + col0 + wc * WTN + lcol;
+      double* crow = Cb + (int64_t)row * p.ldc + col0 + wc * WT + lcol;
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
+      for (int ni = 0; ni < MI; ++ni) {
         double v = p.alpha * acc[mi][ni][r];
         if (p.beta != 0.0) v = fma(p.beta, crow[ni * 16], v);
         crow[ni * 16] = v;
@@ -269,17 +255,14 @@ __device__ void gemm_sk_block(const GemmParams& p, int s, double* smem) {
   }
 }
 
-template <int ALAY, int BLAY, int EPI, int TILE, int NW>
+template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o, int ke_o, double* part) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
-  static_assert(NW == 4 || (NW == 8 && EPI == EPI_STORE && TILE == 128), "8 waves: EPI_STORE 128");
-  constexpr int WT = TILE / 2;           // per-wave sub-tile rows (2 wave rows)
-  constexpr int WTN = TILE * 2 / NW;     // per-wave sub-tile columns (NW/2 wave columns)
-  constexpr int MI = WT / 16;            // MFMA blocks per wave edge (rows)
-  constexpr int NI = WTN / 16;           //                          (columns)
-  constexpr int PER = TILE * BK / (64 * NW);  // doubles of one operand slice per thread (8 or 4)
+  constexpr int WT = TILE / 2;           // per-wave sub-tile edge
+  constexpr int MI = WT / 16;            // MFMA blocks per wave edge
+  constexpr int PER = TILE * BK / 256;   // doubles of one operand slice per thread (8 or 4)
   constexpr int NQ = PER / 2;            // 16-byte loads per operand per thread
   constexpr int TPR = TILE / PER;        // threads per k-row for k-major sources (each thread
                                          // owns NQ 16-byte chunks 2·TPR doubles apart, so a
@@ -294,7 +277,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
   constexpr bool SK = TILE == 64 || (ALAY == LAY_N && BLAY == LAY_T);
   auto rowoff = [](int k) { return k * LS + (SK ? 4 * (k >> 2) : 0); };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / (NW / 2), wc = wave % (NW / 2);
+  const int wr = wave >> 1, wc = wave & 1;
   const int row0 = ti * TILE, col0 = tj * TILE;
 
   int kb = 0, ke = p.K;
@@ -388,11 +371,11 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     }
   };
 
-  d4 acc[MI][NI];
+  d4 acc[MI][MI];
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
+    for (int ni = 0; ni < MI; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
 
   auto compute = [&](int buf) {
     const double* As = smem + buf * STAGE;
@@ -400,15 +383,15 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
       const int krow = rowoff(kk * 4 + (lane >> 4)) + (lane & 15);
-      double a[MI], b[NI];
+      double a[MI], b[MI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) a[mi] = As[krow + wr * WT + mi * 16];
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) b[ni] = Bs[krow + wc * WTN + ni * 16];
+      for (int ni = 0; ni < MI; ++ni) b[ni] = Bs[krow + wc * WT + ni * 16];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
+        for (int ni = 0; ni < MI; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
     }
   };
@@ -450,18 +433,16 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
 
   const int lrow = lane >> 4, lcol = lane & 15;
   if constexpr (EPI == EPI_STORE) {
-    if constexpr (NW == 4) {
-      if (part) {  // stream-K partial: this thread's accumulators, coalesced ([element][thread])
+    if (part) {  // stream-K partial: this thread's accumulators, coalesced ([element][thread])
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
+        for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) part[((mi * MI + ni) * 4 + r) * 256 + tid] = acc[mi][ni][r];
-        return;
-      }
+          for (int r = 0; r < 4; ++r) part[((mi * MI + ni) * 4 + r) * 256 + tid] = acc[mi][ni][r];
+      return;
     }
-    store_acc<TILE, NW>(p, ti, tj, kslice, acc);
+    store_acc<TILE>(p, ti, tj, kslice, acc);
   } else if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
     // out0[tj][row] = sum over this tile's columns of (alpha*acc)^2
     double* red = smem;  // [2 (wc)][TILE rows]
@@ -702,7 +683,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
 int g_stream_k = 1;   // GPS_OPT_STREAM_K (process-wide)
-int g_gemm_waves = 4; // GPS_OPT_GEMM_WAVES (process-wide): 8 = gemm_f64_kernel8 for EPI_STORE 128
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
 static int small_wpt(int K) { return K >= 64 ? 4 : (K >= 32 ? 2 : 1); }
@@ -824,8 +804,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // round of workgroup slots would be at most 3/4 full runs that round's tiles as equal K runs
   // over every slot instead
   q.sk_dp = q.sk_wgs = 0;
-  const bool w8 = g_gemm_waves == 8 && epi == EPI_STORE && tile == 128;
-  if (g_stream_k && !w8 && epi == EPI_STORE && tile == 128 && q.ksplit == 1 && q.sk_cnt && q.ws &&
+  if (g_stream_k && epi == EPI_STORE && tile == 128 && q.ksplit == 1 && q.sk_cnt && q.ws &&
       q.sk_slots > 0 && q.tri == TRI_NONE && (q.lower_out || q.map_mode == 0 || q.map_mode == 2)) {
     const int slots = q.sk_slots, rem = tiles % slots;
     if (tiles >= slots && rem > 0 && 4 * rem <= 3 * slots && rem <= kStreamKTiles &&
@@ -837,16 +816,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   }
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
-  if (w8) {
-#define GPS_GEMM_CASE8(AL, BL)                                                              \
-    if (err == hipErrorInvalidValue && alay == AL && blay == BL) {                          \
-      hipLaunchKernelGGL((gemm_f64_kernel8<AL, BL>), grid, dim3(512), 0, s, q);              \
-      err = hipGetLastError();                                                              \
-    }
-    GPS_GEMM_CASE8(LAY_N, LAY_T) GPS_GEMM_CASE8(LAY_N, LAY_N)
-    GPS_GEMM_CASE8(LAY_T, LAY_N) GPS_GEMM_CASE8(LAY_T, LAY_T)
-#undef GPS_GEMM_CASE8
-  }
 #define GPS_GEMM_CASE(AL, BL, EP, T)                                               \
   if (err == hipErrorInvalidValue && alay == AL && blay == BL && epi == EP && tile == T) { \
     hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T>), grid, block, 0, s, q);   \

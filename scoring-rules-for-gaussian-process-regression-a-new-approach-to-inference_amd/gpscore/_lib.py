@@ -25,7 +25,6 @@ GPS_OPT_DAG_TILES = 13
 GPS_OPT_DAG_GROUP = 17
 GPS_OPT_STREAM_K = 18
 GPS_OPT_DAG_WGS = 19
-GPS_OPT_GEMM_WAVES = 20
 GPS_OPT_FORK_MAX = 14
 GPS_OPT_AR_CHUNKS = 15
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")

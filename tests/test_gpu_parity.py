@@ -682,34 +682,6 @@ def test_persistent_factorisation_matches_recursion(gpu_ctx, n, tiles):
     assert abs(r1.objectives["nlml"] - f["nlml"]) < 1e-9 * abs(f["nlml"])
 
 
-def test_gemm_eight_waves(gpu_ctx):
-    """GPS_OPT_GEMM_WAVES = 8: the plain-store 128-tile GEMMs on 8 waves of 64×32 — every output
-    element is the same MFMA chain in the same k order as with 4 waves of 64×64, so the fit and
-    the predict are bitwise those of the default."""
-    import gpscore
-    from gpscore import _lib
-    rng = np.random.default_rng(21)
-    n, nt, d = 8192, 1000, 6
-    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
-    y = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n)
-    th = (0.2, np.log(1.7) * np.ones(d), np.log(0.02))
-    gp = gpscore.GP(ctx=gpu_ctx)
-    runs = []
-    try:
-        for sk, w in ((0, 4), (0, 8)):  # (the stream-K tail is a 4-wave path: off for both)
-            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_STREAM_K, sk)
-            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_GEMM_WAVES, w)
-            r = gp.fit(X, y, th)
-            mu, var = gp.predict(Xt)
-            runs.append((r, mu, var))
-    finally:
-        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_GEMM_WAVES, 4)
-        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_STREAM_K, 1)
-    (r4, mu4, v4), (r8, mu8, v8) = runs
-    assert r8.objectives == r4.objectives
-    assert np.array_equal(r8.mu_loo, r4.mu_loo) and np.array_equal(mu8, mu4) and np.array_equal(v8, v4)
-
-
 def test_persistent_factorisation_any_grid_bitwise(gpu_ctx):
     """GPS_OPT_DAG_WGS: the queue is a topological order and every task's arithmetic is fixed, so
     4 workgroups (a near-serial drain) and one per CU give the same bits."""
