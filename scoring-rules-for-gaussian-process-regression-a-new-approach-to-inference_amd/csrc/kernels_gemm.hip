@@ -682,7 +682,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 }
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
-int g_stream_k = 1;   // GPS_OPT_STREAM_K (process-wide)
+int g_stream_k = 0;   // GPS_OPT_STREAM_K (process-wide; off: DESIGN §6.20)
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
 static int small_wpt(int K) { return K >= 64 ? 4 : (K >= 32 ? 2 : 1); }

@@ -752,7 +752,7 @@ def test_stream_k_tail(gpu_ctx, n):
             gp.fit(X, y, (0.5, np.log(0.9) * np.ones(d), np.log(0.05)))  # other values first
             runs.append(gp.fit(X, y, th))
     finally:
-        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_STREAM_K, 1)
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_STREAM_K, 0)
     r0, r1, r2 = runs
     assert r1.objectives == r2.objectives
     assert np.array_equal(r1.mu_loo, r2.mu_loo) and np.array_equal(r1.var_loo, r2.var_loo)
