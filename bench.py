@@ -170,6 +170,25 @@ def alg_flop(kind, c, world=1):
 MFMA_TAGS = ("gemm", "potrf_dag")
 
 
+def phases(ctl, ctx, model, theta, steps, prof, ms_unit, upload=None):
+    """each phase of the unit and their sum — fit (Gram, factor, logdet, α,
+    diag A⁻¹ -> NLML / LOO-CRPS / LOO-LogS) and predict (μ*, σ²* and the fused score sums)
+    timed separately on the production path; the score kernels' share from the kernel pass.
+    `upload` (host -> HBM copies of the inputs) gives the PCIe-inclusive end-to-end figure, which
+    is never `value`."""
+    up_ms = 1e3 * timed(ctl, ctx, upload, steps) / steps if upload else None
+    t_fit = timed(ctl, ctx, lambda: model.fit(theta=theta, return_loo=False), steps)
+    t_pred = timed(ctl, ctx, lambda: model.predict(with_scores=True), steps)
+    fit_ms, pred_ms = 1e3 * t_fit / steps, 1e3 * t_pred / steps
+    sc = prof.get("score_sums", {})
+    return {"fit_ms": fit_ms, "predict_ms": pred_ms,
+            "score_ms": sc.get("ms", 0.0) / steps if sc else None,
+            "sum_ms": fit_ms + pred_ms, "unit_ms": ms_unit, "upload_ms": up_ms,
+            "end_to_end_ms": (up_ms + fit_ms + pred_ms) if upload else None,
+            "note": "predict_ms includes the score (fused into the predict call: one launch pair "
+                    "after the finalise); score_ms = those kernels alone (single-stream pass)"}
+
+
 def roofline_mfma(prof, traffic=None, steps=1, flop_alg=None):
     """Every MFMA launch of a step — the GEMMs and the persistent factorisation of the bottom
     diagonal blocks, which carries part of the n³/3 + n³/3: achieved = algorithmic flops
@@ -460,6 +479,10 @@ def main():
     ms_full = 1e3 * t_full / args.steps
     # kernel-accounting pass: same steps, one stream, hipEvents around every launch
     prof, ms_acct = kernel_pass(ctl, ctx, unit, args.steps)
+    def upload():
+        gp.set_data(X, y)
+        gp.set_test(Xt, yt)
+    unit_phases = phases(ctl, ctx, gp, th, args.steps, prof, ms_full, upload)
     got = gpu_unit_outputs(gp, th)  # every output of the unit, for the parity record
     obj = {k: got[k] for k in ("nlml", "loo_crps", "loo_logs", "logdet", "quad")}
     sc = {k: got[k] for k in ("test_crps", "test_logs", "test_msll", "test_smse", "test_mse",
@@ -491,6 +514,7 @@ def main():
         "roofline_trailing_update": roofline_trailing(prof, args.steps),
         "objectives": obj, "scores": sc,
         "kernels_per_step": kernel_summary(prof, args.steps),
+        "phases": unit_phases,
         "kernel_accounting": {"ms_per_step": ms_acct, "streams": 1,
                               "note": "second timed pass, overlap off, hipEvents around each launch"},
     }
@@ -580,6 +604,7 @@ def main():
                 funit()
             tf = timed(ctl, ctx, funit, args.steps)
             fprof, fms_acct = kernel_pass(ctl, ctx, funit, args.steps)
+            fphases = phases(ctl, ctx, fgp, thf, args.steps, fprof, 1e3 * tf / args.steps)
             fobj = fgp.fit(theta=thf, return_loo=False).objectives
             fitc[leg] = {"ms_per_step": 1e3 * tf / args.steps,
                          "units_per_s": args.steps / tf,
@@ -591,6 +616,7 @@ def main():
                              fprof, read_traffic(args.fitc_traffic_json)[0] if leg == "C4" else None,
                              args.steps, alg_flop("fitc", fc, world)),
                          "kernel_accounting_ms_per_step": fms_acct,
+                         "phases": fphases,
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             if not args.no_grad:  # next-1: one FITC GD iteration (theta and Z), K20:222-247
                 fg = {}

@@ -1726,6 +1726,9 @@ int gps_full_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
                            ctx->s2.d(), s));
     HIPCHK(launch_pred_finalize(ctx->s1.d(), ctx->s2.d(), (int)nt, ctx->th.sn2 + ctx->th.sf2,
                                 ctx->mu.d(), ctx->var.d(), s));
+  }
+  {  // the score phase (KF:276-292): its own profiling tag
+    Prof pr(ctx, "score_sums", 0, 24.0 * nt);
     double* part = row_part(ctx, nt, 6);
     ARGCHK(part != nullptr, "out of device memory");
     HIPCHK(launch_score_sums(ctx->mu.d(), ctx->var.d(), ctx->yt.d(), (int)nt, ctx->ytr_mean,
@@ -2833,6 +2836,9 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
     if (nt > 0)  // a rank may hold no test rows; its zero score partials still join the sum
       HIPCHK(launch_fitc_pred_finalize(ctx->qm.d(), ctx->qb.d(), (int)nt, th.sn2 + th.sf2,
                                        ctx->fvar.d(), s));
+  }
+  {  // the score phase (KF:276-292): its own profiling tag
+    Prof pr(ctx, "score_sums", 0, 24.0 * nt);
     double* part = row_part(ctx, nt, 6);
     ARGCHK(part != nullptr, "out of device memory");
     if (nt > 0)
