@@ -163,7 +163,8 @@ struct gps_ctx {
   bool f_data = false, f_test = false, f_z = false, f_fitted = false;
   // test-side ‖Lm⁻¹k_*‖² formed by gps_fitc_fit on aux[0] during Lb's factorisation
   bool f_pre = false;
-  hipEvent_t pre_fork = nullptr, pre_join = nullptr;
+  bool f_pre_b = false;  // ... and ‖Lb⁻¹k_*‖², beside the r pass (fitc_test_prepass_b)
+  hipEvent_t pre_fork = nullptr, pre_join = nullptr, preb_fork = nullptr;
   hipEvent_t kn_fork = nullptr, kn_join = nullptr;  // the FITC Knm Gram beside Lm's factorisation
   DBuf fslab_pre;
   Theta fth;
@@ -1191,7 +1192,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->kn_fork, ctx->kn_join})
+  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->preb_fork, ctx->kn_fork, ctx->kn_join})
     if (e) (void)hipEventDestroy(e);
   for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1758,7 +1759,7 @@ int gps_fitc_set_data(gps_ctx* ctx, const double* X, const double* y, int64_t n,
   if (int rc = upload(ctx, ctx->fy, y, n, 1, ctx->fn_pad)) return rc;
   ctx->f_data = true;
   ctx->f_fitted = false;
-  ctx->f_pre = false;
+  ctx->f_pre = ctx->f_pre_b = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1776,7 +1777,7 @@ int gps_fitc_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t 
   if (!yt) zeros.assign(std::max<int64_t>(nt, 1), 0.0);
   if (int rc = upload(ctx, ctx->fyt, yt ? yt : zeros.data(), nt, 1, ctx->fnt_pad)) return rc;
   ctx->f_test = true;
-  ctx->f_pre = false;
+  ctx->f_pre = ctx->f_pre_b = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1790,7 +1791,7 @@ int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m) {
   if (int rc = upload(ctx, ctx->Z, Z, m, ctx->fd, ctx->m_pad)) return rc;
   ctx->f_z = true;
   ctx->f_fitted = false;
-  ctx->f_pre = false;
+  ctx->f_pre = ctx->f_pre_b = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1942,13 +1943,34 @@ int fitc_test_prepass(gps_ctx* ctx) {
   return 0;
 }
 
+// The other test-side row norms, q*b_i = ‖Lb⁻¹k*_i‖², once Lb⁻¹ is final: on aux[0] (after the
+// q* pass there) while the main stream runs the training r pass, whose last round of workgroup
+// slots they fill; predict then has only μ* and the finalise left (K20:76-83).
+int fitc_test_prepass_b(gps_ctx* ctx) {
+  const int64_t ntp = ctx->fnt_pad, mp = ctx->m_pad, tm = mp / GPS_TILE;
+  hipStream_t a = ctx->aux[0];
+  HIPCHK(ensure(ctx->qb, ntp * 8));
+  if (!ctx->preb_fork) HIPCHK(hipEventCreateWithFlags(&ctx->preb_fork, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ctx->preb_fork, ctx->stream));
+  HIPCHK(hipStreamWaitEvent(a, ctx->preb_fork, 0));
+  GemmParams p = gp0();
+  p.A = ctx->Ksm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp;
+  p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+  p.out0 = ctx->fslab_pre.d(); p.ld_out = ntp;  // (the q* slab sum precedes on aux[0])
+  if (int rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, a)) return rc;
+  HIPCHK(launch_slab_sum(ctx->fslab_pre.d(), ntp, (int)tm, ntp, nullptr, ctx->qb.d(), a));
+  HIPCHK(hipEventRecord(ctx->pre_join, a));
+  ctx->f_pre_b = true;
+  return 0;
+}
+
 // forward FITC objectives; leaves Knm, Lm⁻¹, Lb⁻¹, λ, r, g = Knm c, c on the device.
 // pre_test: also form the test-side Lm row norms during B's factorisation (gps_fitc_fit)
 int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
                   bool pre_test = false) {
   ARGCHK(ctx->f_data && ctx->f_z, "gps_fitc_set_data / gps_fitc_set_inducing first");
   ctx->f_fitted = false;  // set again by the callers once check_info has passed
-  ctx->f_pre = false;
+  ctx->f_pre = ctx->f_pre_b = false;
   if (int rc = set_theta(ctx, ctx->fth, GPS_ARD, theta, n_ell, ctx->fd)) return rc;
   const Theta& th = ctx->fth;
   const int64_t n = ctx->fn, np = ctx->fn_pad, m = ctx->m, mp = ctx->m_pad;
@@ -2073,6 +2095,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                          nullptr, ctx->fslab.d(), s, 32));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
+  if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
   {  // r_i = ‖Lb⁻¹ k_i‖², and g = Knm c from the same pass over Knm (its last column tile)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp;
@@ -2814,6 +2837,7 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   double* sums = ctx->small.d() + 8;
   int rc;
   const bool pre = ctx->f_pre;  // K*m and q* came with the fit (fitc_test_prepass)
+  const int wend = ctx->f_pre_b ? 1 : 2;  // ... and q*b (fitc_test_prepass_b)
   if (pre) {
     HIPCHK(hipStreamWaitEvent(s, ctx->pre_join, 0));
   } else if ((rc = gram(ctx, "gram_ksm", ctx->fXt.d(), (int)nt, ctx->Z.d(), (int)m, ctx->fd, th,
@@ -2822,7 +2846,7 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   }
   const double* Ls[2] = {ctx->Lm.d(), ctx->Lb.d()};
   double* outs[2] = {ctx->qm.d(), ctx->qb.d()};
-  for (int w = pre ? 1 : 0; w < 2; ++w) {
+  for (int w = pre ? 1 : 0; w < wend; ++w) {
     GemmParams p = gp0();
     p.A = ctx->Ksm.d(); p.lda = mp; p.B = Ls[w]; p.ldb = mp;
     p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
