@@ -166,6 +166,7 @@ struct gps_ctx {
   bool f_pre_b = false;  // ... and ‖Lb⁻¹k_*‖², beside the r pass (fitc_test_prepass_b)
   hipEvent_t pre_fork = nullptr, pre_join = nullptr, preb_fork = nullptr;
   hipEvent_t kn_fork = nullptr, kn_join = nullptr;  // the FITC Knm Gram beside Lm's factorisation
+  hipEvent_t b_fork = nullptr, b_join = nullptr;    // the FITC b pass beside B's SYRK
   DBuf fslab_pre;
   Theta fth;
   // ---- comm: RCCL (gps_comm_init) or the in-process group (gps_comm_init_local)
@@ -1192,7 +1193,8 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->preb_fork, ctx->kn_fork, ctx->kn_join})
+  for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->preb_fork, ctx->kn_fork, ctx->kn_join,
+                       ctx->b_fork, ctx->b_join})
     if (e) (void)hipEventDestroy(e);
   for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -2062,18 +2064,31 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                               th.sn2, ctx->q.d(), ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal,
                               part, s));
   }
-  {  // b_p = Kmnᵀ Λ⁻¹ y
-    Prof pr(ctx, "colred_b", 0, 8.0 * np * mp);
-    HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ctx->ys.d(), nullptr, bvec,
-                         nullptr, ctx->fslab.d(), s));
+  // b_p = Kmnᵀ Λ⁻¹ y: one rank, an HBM-bound pass on aux[1] beside the SYRK (b is first read
+  // by c = B⁻¹b after B's factorisation); sharded, it travels in the all-reduce with B
+  const bool bside = !shard && ctx->overlap && !ctx->prof;
+  if (bside) {
+    for (hipEvent_t* e : {&ctx->b_fork, &ctx->b_join})
+      if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->b_fork, s));
+    HIPCHK(hipStreamWaitEvent(ctx->aux[1], ctx->b_fork, 0));
   }
+  {
+    hipStream_t bs = bside ? ctx->aux[1] : s;
+    Prof pr(ctx, "colred_b", 0, 8.0 * np * mp, bs);
+    HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ctx->ys.d(), nullptr, bvec,
+                         nullptr, ctx->fslab.d(), bs));
+  }
+  if (bside) HIPCHK(hipEventRecord(ctx->b_join, ctx->aux[1]));
   // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs); sharded: packed and all-reduced with b,
   // Σlogλ, Σy²/λ, in row blocks overlapped with the SYRK (ctx->ar_chunks)
   if (shard) {
     if ((rc = fitc_syrk_allreduce(ctx, red, blen, mp + 2))) return rc;
   } else if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc, false))) {
+    if (bside) (void)hipStreamWaitEvent(s, ctx->b_join, 0);
     return rc;
   }
+  if (bside) HIPCHK(hipStreamWaitEvent(s, ctx->b_join, 0));
   if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
     if ((rc = fitc_test_prepass(ctx))) return rc;
   // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
