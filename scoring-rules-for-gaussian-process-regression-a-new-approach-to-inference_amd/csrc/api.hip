@@ -2009,10 +2009,11 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   const int64_t red_len = mp * mp + mp + 8;
   HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
   const int64_t nchunk = (std::max(np, mp) + 255) / 256;
-  // (row-norm partials tm·np; column passes' chunk partials: Knm's 256-row chunks, and the
-  //  m×m pass for c in 32-row chunks)
+  // (row-norm partials tm·np; column passes' chunk partials: Knm's 256-row chunks, and, after
+  //  the r pass's first column tiles (formed during B's factorisation), the m×m pass for c in
+  //  32-row chunks)
   const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * np, nchunk * mp * 2),
-                                              (mp + 31) / 32 * mp);
+                                              tm * np + (mp + 31) / 32 * mp);
   HIPCHK(ensure(ctx->fslab, (size_t)fslab_len * 8));
   double* red = ctx->red.d();
   double* Bacc = red;
@@ -2096,9 +2097,14 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
   else
     HIPCHK(launch_sym_slab_sum(Bacc, 0, 1, (int)mp, ctx->Kmm.d(), ctx->Am.d(), s));
+  // (the r pass's column tiles [0, qn1), like q's, as soon as the top-level Lb11⁻¹ is final)
+  ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
+  ctx->pre.n1 = qn1;
+  ctx->pre.L = ctx->Lb.d();
   ctx->dag_half = true;
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr);
   ctx->dag_half = false;
+  ctx->pre.kind = PRE_NONE;
   if (rc) return rc;
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
   {  // c = Lb⁻ᵀ Lb⁻¹ b
@@ -2107,15 +2113,16 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     // (32-row chunks: an m×m pass has few 256-row chunks, 32 workgroups at m = 2048; fslab
     //  holds the m/32 chunk partials)
     HIPCHK(launch_colred(ctx->Lb.d(), mp, (int)mp, (int)mp, 1, ctx->tvec.d(), nullptr, ctx->c.d(),
-                         nullptr, ctx->fslab.d(), s, 32));
+                         nullptr, ctx->fslab.d() + tm * np, s, 32));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
   if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
-  {  // r_i = ‖Lb⁻¹ k_i‖², and g = Knm c from the same pass over Knm (its last column tile)
+  {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation), and
+     // g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
     GemmParams p = gp0();
-    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp;
-    p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
-    p.out0 = ctx->fslab.d(); p.ld_out = np;
+    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d() + qn1 * mp; p.ldb = mp;
+    p.M = (int)np; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
+    p.out0 = ctx->fslab.d() + (qn1 / GPS_TILE) * np; p.ld_out = np;
     p.w = ctx->c.d(); p.out1 = ctx->g.d();
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ_DOT, p))) return rc;
   }

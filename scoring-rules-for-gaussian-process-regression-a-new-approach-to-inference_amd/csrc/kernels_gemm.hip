@@ -734,9 +734,11 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   if ((p.lda & 1) || (p.ldb & 1) || (p.ldc & 1)) return hipErrorInvalidValue;
   if (p.lower_out && p.M != p.N) return hipErrorInvalidValue;
   if (p.ksplit < 1) p.ksplit = 1;
-  // the row dot comes from the last column tile, which must span the whole K range
+  // the row dot comes from the last column tile, which must span the whole K range (columns
+  // [tri_off, tri_off + N) of a larger triangular product whose last column is K)
   if (epi == EPI_ROWSQ_DOT &&
-      (!p.w || !p.out1 || p.tri != TRI_K_LE_J || p.tri_off != 0 || p.K != p.N || p.ksplit != 1))
+      (!p.w || !p.out1 || p.tri != TRI_K_LE_J || p.tri_off < 0 || p.K != p.tri_off + p.N ||
+       p.ksplit != 1))
     return hipErrorInvalidValue;
   const GemmPlan plan = gemm_plan(epi, p, p.ws ? p.ws_cap : 0);
   const int tile = plan.tile;

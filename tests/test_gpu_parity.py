@@ -310,10 +310,13 @@ def test_stream_schedules_agree(gp, gpu_ctx):
 
 def test_fitc_q_prepass_matches(gp, gpu_ctx):
     """GPS_OPT_PRED_PRE for FITC: the q_i = ‖Lm⁻¹k_i‖² column tiles [0, n1) run on aux[0]
-    during Lm's factorisation, the rest after it — same tiles and K ranges as one launch, so
-    fit, LOO vectors and predictives agree to 1e-14 with the option off (and with the oracle)."""
+    during Lm's factorisation and the r_i = ‖Lb⁻¹k_i‖² ones during B's, the rest after each —
+    same tiles and K ranges as one launch (the r pass's row dot g = Knm c from its last column
+    tile either way), so fit, LOO vectors and predictives agree to 1e-14 with the option off
+    (and with the oracle).  m = 2700: 22 tiles, above the 20-tile persistent block, so the
+    factorisations recurse once and the pre-passes exist."""
     rng = np.random.default_rng(13)
-    n, nt, m, d = 9000, 700, 1100, 8
+    n, nt, m, d = 9000, 700, 2700, 8
     X, Xt = rng.standard_normal((n, d)), rng.standard_normal((nt, d))
     Z = X[rng.choice(n, m, replace=False)]
     y, yt = np.sin(X.sum(1)), np.sin(Xt.sum(1))
