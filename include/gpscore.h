@@ -191,7 +191,10 @@ int gps_fitc_set_test(gps_ctx* ctx, const double* Xt, const double* yt, int64_t 
 int gps_fitc_set_inducing(gps_ctx* ctx, const double* Z, int64_t m);
 /* FITC objectives over this rank's rows.  With a communicator (gps_comm_init)
  * the m×m accumulator and scalar partials are all-reduced over RCCL; objectives
- * are then global and mu_loo / var_loo hold this rank's rows. */
+ * are then global and mu_loo / var_loo hold this rank's rows.  With a test set resident
+ * (gps_fitc_set_test) and GPS_OPT_OVERLAP on, the fit also forms the test-side row norms
+ * ‖Lm⁻¹k*‖² and ‖Lb⁻¹k*‖² on a second stream where its own chain leaves the chip idle, so
+ * gps_fitc_predict is left with μ* and the finalise; a new test set voids them. */
 int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_OBJ],
                  double* mu_loo, double* var_loo);
 /* Forward + analytic gradient of one FITC objective w.r.t. theta AND the inducing
