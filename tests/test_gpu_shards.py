@@ -137,6 +137,18 @@ def test_fitc_shards_match_unsharded(gpu_ctx, P):
              f"fitc_shards_P{P}")
 
 
+def test_fitc_shards_large_m(gpu_ctx):
+    """m = 2700 (22 tiles: the m×m factorisations recurse once, so the q and r row-norm passes
+    each have a pre-pass on a second stream inside the captured factorisation, and the fit
+    forms the test-side row norms), 2 shards, forward + predict: within 30× the floor."""
+    X, y, Xt, yt, Z, th = _case(7001, 1201, 2700, 16, 44)  # d = 16: cond(K̃mm) ~3e3
+    ref = _whole(X, y, Xt, yt, Z, th, False, gpu_ctx)
+    parts = _sharded(2, X, y, Xt, yt, Z, th, False)
+    from test_gpu_parity import fitc_cap
+    _compare(parts, ref, _floor(X, y, Xt, yt, Z, th, False, gpu_ctx, ref), fitc_cap(Z, th),
+             "fitc_shards_large_m")
+
+
 def test_fitc_shards_golden(gpu_ctx):
     """The reference-pinned golden case, 3 shards: same objectives as the dense reference."""
     g = load_golden("fitc_n2000_m200_rows")
