@@ -116,11 +116,24 @@ __device__ __forceinline__ void tile_update2(double* S, int d0, int a0, int d1, 
   for (int q = 0; q < 4; ++q) { S[acc_off(d0, lane, q)] = c0[q]; S[acc_off(d1, lane, q)] = c1[q]; }
 }
 
+// lane c of every 16-lane row gets x from lane C of its own row (v_mov_b64 row_newbcast:C)
+template <int C>
+__device__ __forceinline__ double row_bcast(double x) {
+  long long v = __double_as_longlong(x), old = 0;
+  return __longlong_as_double(__builtin_amdgcn_update_dpp(old, v, 0x150 + C, 0xf, 0xf, true));
+}
+
 // pivot wave: factor panel p held in P (rows l + 64 s), diagonal tile in row slot DS; LO:
-// slot 0 holds panel rows
+// slot 0 holds panel rows.  Per column j: the pivot by v_readlane, v_rsq_f64 + one Newton step;
+// the next column's multiplier (the dependent chain) by v_readlane; the rest of column j's
+// multipliers L[J0+c][j] from ONE copy of the diagonal tile's column in every 16-lane row
+// (two ds_bpermute) and a 64-bit DPP row broadcast each — the v_readlane pair per multiplier
+// this replaces was the panel's issue bound (tools/panel_probe.hip v7 vs v8: 3.8k vs 4.3k cycles
+// with one row slot).  Every element gets the same FMAs in the same order: bitwise the same L.
 template <int DS, bool LO>
 __device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane) {
   const int J0 = 16 * p;
+  const int src = 4 * ((J0 & 63) + (lane & 15));  // bpermute byte address: the diagonal row
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int J = J0 + j;
@@ -136,18 +149,23 @@ __device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane
       const double v = P[s][j] * rs;
       P[s][j] = R > J ? v : (R == J ? ljj : 0.0);
     }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    double m1 = 0.0;
-    if (j < 15) m1 = rl(P[DS][j], (J + 1) & 63);
+    if (j == 15) break;
+    const double pj = P[DS][j];
+    const int clo = __builtin_amdgcn_ds_bpermute(src, __double2loint(pj));
+    const int chi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(pj));
+    const double m1 = rl(pj, (J + 1) & 63);
 #pragma unroll
-    for (int c = j + 1; c < 16; ++c) {
-      const double m = c == j + 1 ? m1 : rl(P[DS][j], (J0 + c) & 63);
-#pragma unroll
-      for (int s = LO ? 0 : 1; s < 2; ++s) P[s][c] = fma(-P[s][j], m, P[s][c]);
+    for (int s = LO ? 0 : 1; s < 2; ++s) P[s][j + 1] = fma(-P[s][j], m1, P[s][j + 1]);
+    const double col = __hiloint2double(chi, clo);
+#define GPS_PANEL_UPD(C)                                                                  \
+    if (C > j + 1) {                                                                      \
+      const double m = row_bcast<C>(col);                                                 \
+      _Pragma("unroll") for (int s = LO ? 0 : 1; s < 2; ++s) P[s][C] = fma(-P[s][j], m, P[s][C]); \
     }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
+    GPS_PANEL_UPD(2) GPS_PANEL_UPD(3) GPS_PANEL_UPD(4) GPS_PANEL_UPD(5) GPS_PANEL_UPD(6)
+    GPS_PANEL_UPD(7) GPS_PANEL_UPD(8) GPS_PANEL_UPD(9) GPS_PANEL_UPD(10) GPS_PANEL_UPD(11)
+    GPS_PANEL_UPD(12) GPS_PANEL_UPD(13) GPS_PANEL_UPD(14) GPS_PANEL_UPD(15)
+#undef GPS_PANEL_UPD
   }
 }
 

@@ -82,6 +82,83 @@ __device__ __forceinline__ void factor_panel_lds(double (&P)[2][16], int J0, int
   if (EXTRA && badp) *badp = bad;
 }
 
+// variant 7: the diagonal tile's column j replicated to all four 16-lane rows by ds_bpermute
+// (two per column), then each multiplier L[J0+c][j] taken by a 64-bit DPP row_newbcast:c of that
+// copy — no v_readlane pair (and its SGPR hazards) per multiplier; the chain's next pivot column
+// (c = j+1) keeps its v_readlane.  Same FMAs in the same order per element: bitwise equal to v2.
+template <int C>
+__device__ __forceinline__ double nbcast(double x) {
+  long long v = __double_as_longlong(x), old = 0;
+  long long r = __builtin_amdgcn_update_dpp(old, v, 0x150 + C, 0xf, 0xf, true);
+  return __longlong_as_double(r);
+}
+template <int DS, bool LO>
+__device__ __forceinline__ void factor_panel_dpp(double (&P)[2][16], int J0, int l) {
+  const int src = 4 * ((J0 & 63) + (l & 15));  // bpermute byte address: the diagonal row's lane
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int J = J0 + j, lJ = J & 63;
+    const double d = rl(P[DS][j], lJ);
+    const double y = __builtin_amdgcn_rsq(d);
+    const double rs = y * fma(-0.5 * d * y, y, 1.5);
+    const double ljj = d * rs;
+#pragma unroll
+    for (int s = LO ? 0 : 1; s < 2; ++s) {
+      const int R = l + 64 * s;
+      const double v = P[s][j] * rs;
+      P[s][j] = R > J ? v : (R == J ? ljj : 0.0);
+    }
+    if (j == 15) break;
+    const double pj = P[DS][j];
+    const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(pj));
+    const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(pj));
+    const double m1 = rl(pj, (J + 1) & 63);
+#pragma unroll
+    for (int s = LO ? 0 : 1; s < 2; ++s) P[s][j + 1] = fma(-P[s][j], m1, P[s][j + 1]);
+    const double Mrep = __hiloint2double(hi, lo);
+#define GPS_UPD(C)                                                                     \
+    if (C > j + 1) {                                                                   \
+      const double m = nbcast<C>(Mrep);                                                \
+      _Pragma("unroll") for (int s = LO ? 0 : 1; s < 2; ++s) P[s][C] = fma(-P[s][j], m, P[s][C]); \
+    }
+    GPS_UPD(2) GPS_UPD(3) GPS_UPD(4) GPS_UPD(5) GPS_UPD(6) GPS_UPD(7) GPS_UPD(8) GPS_UPD(9)
+    GPS_UPD(10) GPS_UPD(11) GPS_UPD(12) GPS_UPD(13) GPS_UPD(14) GPS_UPD(15)
+#undef GPS_UPD
+  }
+}
+
+// variant 8: the library's factor_panel as built (csrc/kernels_potrf.hip v4::factor_panel:
+// v_readlane multipliers, v_rsq_f64 + one Newton step, wave barriers between the phases)
+template <int DS, bool LO>
+__device__ __forceinline__ void factor_panel_lib(double (&P)[2][16], int J0, int lane) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int J = J0 + j;
+    const double d = rl(P[DS][j], J & 63);
+    const double y = __builtin_amdgcn_rsq(d);
+    const double rs = y * fma(-0.5 * d * y, y, 1.5);
+    const double ljj = d * rs;
+#pragma unroll
+    for (int s = LO ? 0 : 1; s < 2; ++s) {
+      const int R = lane + 64 * s;
+      const double v = P[s][j] * rs;
+      P[s][j] = R > J ? v : (R == J ? ljj : 0.0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    double m1 = 0.0;
+    if (j < 15) m1 = rl(P[DS][j], (J + 1) & 63);
+#pragma unroll
+    for (int c = j + 1; c < 16; ++c) {
+      const double m = c == j + 1 ? m1 : rl(P[DS][j], (J0 + c) & 63);
+#pragma unroll
+      for (int s = LO ? 0 : 1; s < 2; ++s) P[s][c] = fma(-P[s][j], m, P[s][c]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
 template <int V>
 __global__ __launch_bounds__(64) void panel_kernel(const double* in, double* out, long long* cyc, int p) {
   const int l = threadIdx.x;
@@ -125,6 +202,12 @@ __global__ __launch_bounds__(64) void panel_kernel(const double* in, double* out
   } else if (V == 2) {
     if (p < 4) factor_panel<0, true>(P, J0, l);
     else factor_panel<1, false>(P, J0, l);
+  } else if (V == 8) {
+    if (p < 4) factor_panel_lib<0, true>(P, J0, l);
+    else factor_panel_lib<1, false>(P, J0, l);
+  } else if (V == 7) {
+    if (p < 4) factor_panel_dpp<0, true>(P, J0, l);
+    else factor_panel_dpp<1, false>(P, J0, l);
   } else if (V <= 4) {
     __shared__ double M[32];
     if (p < 4) factor_panel_lds<0, true, V == 4>(P, J0, l, M);
@@ -157,7 +240,7 @@ int main() {
   double *in, *out; long long* cyc;
   (void)hipMalloc(&in, sizeof(h)); (void)hipMalloc(&out, sizeof(h)); (void)hipMalloc(&cyc, 24);
   (void)hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice);
-  for (int v : {2, 4, 5, 6})
+  for (int v : {8, 7})
     for (int p : {0, 3, 4, 7}) {
       long long best[2] = {1ll << 60, 0};
       for (int rep = 0; rep < 20; ++rep) {
@@ -166,6 +249,8 @@ int main() {
         else if (v == 3) panel_kernel<3><<<1, 64>>>(in, out, cyc, p);
         else if (v == 4) panel_kernel<4><<<1, 64>>>(in, out, cyc, p);
         else if (v == 5) panel_kernel<5><<<1, 64>>>(in, out, cyc, p);
+        else if (v == 7) panel_kernel<7><<<1, 64>>>(in, out, cyc, p);
+        else if (v == 8) panel_kernel<8><<<1, 64>>>(in, out, cyc, p);
         else panel_kernel<6><<<1, 64>>>(in, out, cyc, p);
         long long c[2]; (void)hipMemcpy(c, cyc, 16, hipMemcpyDeviceToHost);
         if (c[0] < best[0]) { best[0] = c[0]; best[1] = c[1]; }
@@ -177,10 +262,10 @@ int main() {
       double err = 0.0;
       for (int i = 0; i < 128 * 16; ++i) {
         if (i / 16 < 16 * p) continue;  // rows above the panel's diagonal tile: unused
-        if (v == 2) ref[pi][i] = o[i];
+        if (v == 8) ref[pi][i] = o[i];
         else err = fmax(err, fabs(o[i] - ref[pi][i]));
       }
-      printf("variant %d panel p=%d: %lld cycles (%lld ns)  max|diff vs v1| %.1e\n", v, p, best[0], best[1] * 10, err);
+      printf("variant %d panel p=%d: %lld cycles (%lld ns)  max|diff vs v8| %.1e\n", v, p, best[0], best[1] * 10, err);
     }
   return 0;
 }
