@@ -71,6 +71,54 @@ def dist_env():
     return world, rank, local
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher's WORLD_SIZE: start N rank processes of this same
+    script (one per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free
+    MASTER_PORT) and wait on them.  This parent only spawns and collects: it never imports torch or
+    gpscore and never touches the GPU (children are started as new processes, not by exec).  The
+    one JSON line comes from rank 0's stdout, which the children share with this process.  If a
+    rank fails, the others are terminated and the first non-zero exit status is returned."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    kill_at = None
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"[bench] rank {procs.index(p)} exited with status {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+                kill_at = time.time() + 30.0  # a rank stuck in a collective may ignore SIGTERM
+        if kill_at is not None and time.time() > kill_at:
+            for q in live:
+                q.kill()
+            kill_at = None
+        time.sleep(0.2)
+    return rc
+
+
 class Ctl:
     """Control plane: barrier and max-over-ranks (gloo on the host; the data-path
     collective is RCCL inside libgpscore)."""
@@ -450,10 +498,40 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
                          "no RCCL communicator (FITC objectives then cover the local shard only)")
+    ap.add_argument("--dry", action="store_true",
+                    help="launcher / control-plane check: ranks meet over gloo, agree on the world "
+                         "size and print the JSON skeleton without touching the GPU")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    # --gpus N with no launcher around us: this process becomes the spawner, before any GPU call
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, local = dist_env()
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
+              f"{world}-process run as {args.gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry and os.environ.get("GPS_BENCH_DRY_FAIL") == str(rank):
+        sys.exit(3)  # launcher test: one rank dies before the control plane forms
     ctl = Ctl(world)
+    if args.dry:
+        # every rank reports its (rank, local rank) over the control plane; rank 0 checks the set
+        me = [rank, local, os.getpid()]
+        everyone = [me]
+        if ctl.dist:
+            everyone = [None] * world
+            ctl.dist.all_gather_object(everyone, me)
+        if rank == 0:
+            ok = sorted(r for r, _, _ in everyone) == list(range(world)) and \
+                len({p for _, _, p in everyone}) == world
+            print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
+                              "ranks": everyone, "ranks_ok": ok, "steps": args.steps,
+                              "warmup": args.warmup}))
+        if ctl.dist:
+            ctl.dist.destroy_process_group()
+        return
     import gpscore
     ctx = gpscore.Context(0 if args.rehearse else local)
     if args.no_tiny_gemm:

@@ -116,12 +116,15 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
 /* Context statistics: out[GPS_STAT_GRAPHS] factorisation graphs cached (one per distinct
  * (buffers, size, streams, options); each holds its instantiated launch sequence, ~1-3 MB of
- * host memory and a few KB of device memory, until the context is destroyed),
- * out[GPS_STAT_GRAPH_CAP] the cache's capacity, out[GPS_STAT_GRAPH_OVERFLOW] factorisations
- * that ran as eager launches because the cache was full (same results, more host time),
- * out[GPS_STAT_DEVICE_BYTES] device memory held by the context's buffers. */
+ * host memory and a few KB of device memory), out[GPS_STAT_GRAPH_CAP] the cache's capacity
+ * (least recently used exec destroyed beyond it), out[GPS_STAT_GRAPH_OVERFLOW] 0 (kept for the
+ * layout: no factorisation runs eagerly for want of a slot), out[GPS_STAT_DEVICE_BYTES] device
+ * memory held by the context's buffers, out[GPS_STAT_GRAPH_DROPPED] execs destroyed because a
+ * buffer they use was freed or grown (a graph never outlives its buffers),
+ * out[GPS_STAT_GRAPH_EVICTED] execs destroyed by the capacity limit. */
 enum { GPS_STAT_GRAPHS = 0, GPS_STAT_GRAPH_CAP = 1, GPS_STAT_GRAPH_OVERFLOW = 2,
-       GPS_STAT_DEVICE_BYTES = 3, GPS_N_STATS = 4 };
+       GPS_STAT_DEVICE_BYTES = 3, GPS_STAT_GRAPH_DROPPED = 4, GPS_STAT_GRAPH_EVICTED = 5,
+       GPS_N_STATS = 6 };
 int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
 
 /* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one

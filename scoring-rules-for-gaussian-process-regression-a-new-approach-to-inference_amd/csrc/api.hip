@@ -119,10 +119,14 @@ struct gps_ctx {
   struct PotrfGraph {                  // one captured potrf_inv launch sequence
     std::vector<uintptr_t> key;
     hipGraphExec_t exec = nullptr;
+    uint64_t last_use = 0;
   };
-  std::vector<PotrfGraph> pgraphs;     // keyed by buffers, sizes, streams, options; kept until
-                                       // the context is destroyed (potrf_inv: kMaxGraphs)
-  int64_t graph_overflow = 0;          // factorisations run eagerly because the cache was full
+  std::vector<PotrfGraph> pgraphs;     // keyed by buffers, sizes, streams, options; least recently
+                                       // used evicted past kMaxGraphs; dropped with their buffers
+  uint64_t graph_tick = 0;
+  int64_t graph_overflow = 0;          // (kept for the stats layout: always 0 since round 4)
+  int64_t graph_dropped = 0;           // execs destroyed because a buffer they bake in was freed
+  int64_t graph_evicted = 0;           // execs destroyed by the LRU cap
   std::string err;
   // profiling
   int prof = 0;  // 1: per-tag timing, 2: per-shape tags
@@ -208,11 +212,49 @@ int fail(gps_ctx* ctx, int code, const std::string& msg) {
     if (!(cond)) return fail(ctx, -1, msg); \
   } while (0)
 
-hipError_t ensure(DBuf& b, size_t bytes) {
+// A cached factorisation graph bakes in the device addresses of the buffers its launches use
+// (every one of them is in its key).  No graph may outlive such a buffer: before a buffer is
+// freed (grown by ensure, or released), every graph whose key holds an address inside it is
+// destroyed — after this context's streams drain, so none is in flight.  (Round 3 kept graphs
+// alive for the context's lifetime instead, after destroying an exec that referenced freed
+// buffers segfaulted the host and a replay read stale counters)
+hipError_t sync_ctx_streams(gps_ctx* ctx) {
+  for (hipStream_t st : {ctx->stream, ctx->side, ctx->aux[0], ctx->aux[1]})
+    if (st) {
+      const hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
+}
+
+hipError_t drop_graphs_in(gps_ctx* ctx, const void* p, size_t bytes) {
+  if (!ctx || !p || ctx->pgraphs.empty()) return hipSuccess;
+  const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+  bool synced = false;
+  for (size_t i = 0; i < ctx->pgraphs.size();) {
+    bool hit = false;
+    for (uintptr_t v : ctx->pgraphs[i].key) hit |= v >= lo && v < hi;
+    if (!hit) { ++i; continue; }
+    if (!synced) {
+      const hipError_t e = sync_ctx_streams(ctx);
+      if (e != hipSuccess) return e;
+      synced = true;
+    }
+    const hipError_t e = hipGraphExecDestroy(ctx->pgraphs[i].exec);
+    ctx->pgraphs.erase(ctx->pgraphs.begin() + (ptrdiff_t)i);
+    ++ctx->graph_dropped;
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t ensure(gps_ctx* ctx, DBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return hipSuccess;
   if (b.p) {
-    hipError_t e = hipFree(b.p);
+    hipError_t e = drop_graphs_in(ctx, b.p, b.cap);
+    if (e != hipSuccess) return e;
+    e = hipFree(b.p);
     if (e != hipSuccess) return e;
   }
   b.p = nullptr;
@@ -221,8 +263,11 @@ hipError_t ensure(DBuf& b, size_t bytes) {
   if (e == hipSuccess) b.cap = bytes;
   return e;
 }
-void release(DBuf& b) {
-  if (b.p) (void)hipFree(b.p);
+void release(gps_ctx* ctx, DBuf& b) {
+  if (b.p) {
+    (void)drop_graphs_in(ctx, b.p, b.cap);
+    (void)hipFree(b.p);
+  }
   b.p = nullptr;
   b.cap = 0;
 }
@@ -321,7 +366,7 @@ int gemm(gps_ctx* ctx, int al, int bl, int epi, const GemmParams& p, hipStream_t
                : st == ctx->aux[0] ? ctx->ws_aux[0]
                : st == ctx->aux[1] ? ctx->ws_aux[1]
                                    : ctx->ws_main;
-    HIPCHK(ensure(ws, (size_t)kSplitWsDoubles * 8));
+    HIPCHK(ensure(ctx, ws, (size_t)kSplitWsDoubles * 8));
     q.ws = ws.d();
     q.ws_cap = kSplitWsDoubles;
     if (st == ctx->stream && ctx->sk_cnt.p) {  // the stream-K tail's tickets (main stream only)
@@ -550,7 +595,7 @@ int reset_info(gps_ctx* ctx) {  // [first non-PD minor, persistent-kernel error]
 // became the bound.  With GPS_OPT_GRAPH (default) the whole sequence is captured once per
 // (buffers, sizes, streams, options) into a hipGraph and replayed with one launch; the
 // eager path remains for profiling (per-launch events) and as the option's off state.
-constexpr size_t kMaxGraphs = 256;
+constexpr size_t kMaxGraphs = 64;
 
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
@@ -568,7 +613,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
     if (ctx->dag_lists.count(T)) continue;
     const std::vector<uint32_t> tl = dag_task_list(T);
     auto& e = ctx->dag_lists[T];
-    HIPCHK(ensure(e.first, tl.size() * 4));
+    HIPCHK(ensure(ctx, e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
     // capturing a graph on its own thread, and a legacy-stream call then fails)
     HIPCHK(hipMemcpyAsync(e.first.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -577,7 +622,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   }
   if (dcnt && ctx->dag_cnt.cap < (size_t)dcnt * 4) {
     HIPCHK(hipStreamSynchronize(ctx->stream));  // no launch of this context still uses the old one
-    HIPCHK(ensure(ctx->dag_cnt, std::max<size_t>((size_t)dcnt * 4, (size_t)1 << 20)));
+    HIPCHK(ensure(ctx, ctx->dag_cnt, std::max<size_t>((size_t)dcnt * 4, (size_t)1 << 20)));
     HIPCHK(hipMemsetAsync(ctx->dag_cnt.p, 0, ctx->dag_cnt.cap, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
@@ -591,10 +636,10 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   if (!ctx->graphs || ctx->prof || n_pad <= GPS_TILE) return eager();
   // capture: everything the recursion allocates must exist beforehand (no allocation inside a
   // capture), and the key names the buffers the sequence bakes in: the split-K workspaces first
-  HIPCHK(ensure(ctx->ws_main, (size_t)kSplitWsDoubles * 8));
-  HIPCHK(ensure(ctx->ws_side, (size_t)kSplitWsDoubles * 8));
+  HIPCHK(ensure(ctx, ctx->ws_main, (size_t)kSplitWsDoubles * 8));
+  HIPCHK(ensure(ctx, ctx->ws_side, (size_t)kSplitWsDoubles * 8));
   const bool pre = ctx->pre.kind == PRE_FITC_Q;
-  const std::vector<uintptr_t> key = {
+  std::vector<uintptr_t> key = {
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
       (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->fork_max, (uintptr_t)ctx->gemm_map,
@@ -605,20 +650,26 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
       (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_half,
-      (uintptr_t)ctx->dag_cnt.p};
+      (uintptr_t)ctx->dag_cnt.p, (uintptr_t)ctx->sk_cnt.p};
+  for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[T].first.p);  // the task lists
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
+      g.last_use = ++ctx->graph_tick;
       HIPCHK(hipGraphLaunch(g.exec, ctx->stream));
       return 0;
     }
-  // Graphs are never destroyed while the context lives: with the HIP runtime that PyTorch
-  // bundles (ROCm 7.0, which serves this library whenever torch is imported first), destroying
-  // a replayed graph exec — even after a device synchronize — made the next capture / replay
-  // segfault on the host (GPU suite, FITC gradient after ~60 cached shapes; a 64-entry cache or
-  // eager launches did not crash).  Past kMaxGraphs shapes the factorisation runs eagerly.
+  // Full cache: the least recently used exec is destroyed (after the context's streams drain).
+  // Every buffer it bakes in is still allocated — a buffer is never freed while a graph that
+  // uses it lives (drop_graphs_in) — which is what round 3's host segfault on destroy lacked.
   if (ctx->pgraphs.size() >= kMaxGraphs) {
-    ++ctx->graph_overflow;
-    return eager();
+    size_t lru = 0;
+    for (size_t i = 1; i < ctx->pgraphs.size(); ++i)
+      if (ctx->pgraphs[i].last_use < ctx->pgraphs[lru].last_use) lru = i;
+    HIPCHK(sync_ctx_streams(ctx));
+    const hipError_t e = hipGraphExecDestroy(ctx->pgraphs[lru].exec);
+    ctx->pgraphs.erase(ctx->pgraphs.begin() + (ptrdiff_t)lru);
+    ++ctx->graph_evicted;
+    HIPCHK(e);
   }
   // ... and the fork/join event pool
   const size_t nev = 2 * (size_t)(n_pad / GPS_TILE) + 8;
@@ -640,7 +691,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   HIPCHK(ei);
-  ctx->pgraphs.push_back({key, exec});
+  ctx->pgraphs.push_back({key, exec, ++ctx->graph_tick});
   HIPCHK(hipGraphLaunch(exec, ctx->stream));
   return 0;
 }
@@ -648,6 +699,9 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
 int check_info(gps_ctx* ctx) {
   HIPCHK(hipMemcpyAsync(ctx->hinfo, ctx->info.p, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->hinfo[1] == 2)
+    return fail(ctx, -4, "persistent factorisation: the task queue did not run to completion "
+                         "(counters not zero at launch; internal error)");
   if (ctx->hinfo[1] != 0x7f7f7f7f)
     return fail(ctx, -4, "persistent factorisation: a task's dependency wait timed out (internal error)");
   const int info = *ctx->hinfo;
@@ -675,7 +729,7 @@ int set_theta(gps_ctx* ctx, Theta& th, int kind, const double* theta, int n_ell,
 }
 
 int upload(gps_ctx* ctx, DBuf& b, const double* h, int64_t rows, int64_t cols, int64_t rows_pad) {
-  HIPCHK(ensure(b, (size_t)rows_pad * cols * 8));
+  HIPCHK(ensure(ctx, b, (size_t)rows_pad * cols * 8));
   HIPCHK(hipMemsetAsync(b.p, 0, (size_t)rows_pad * cols * 8, ctx->stream));
   if (rows * cols)
     HIPCHK(hipMemcpyAsync(b.p, h, (size_t)rows * cols * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -841,7 +895,7 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   const bool stored = nstore && nstore * bp * bp * 8 <= ((size_t)16 << 30);
   const size_t need = (size_t)(6 * Sp * bp + Sp * Sp + 2 * Sp + bp + 8) +
                       ((size_t)nmat + (stored ? nstore : 0)) * bp * bp;
-  HIPCHK(ensure(eb, need * 8));
+  HIPCHK(ensure(ctx, eb, need * 8));
   double* q = eb.d();
   auto take = [&](int64_t cnt) {
     double* t = q;
@@ -995,18 +1049,18 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   hipStream_t s = ctx->stream;
   const int nfold = (int)bnd.size() - 1;
   const int64_t bp = bounds_pad(bnd);
-  HIPCHK(ensure(ctx->bP, (size_t)bp * bp * 8));
+  HIPCHK(ensure(ctx, ctx->bP, (size_t)bp * bp * 8));
   if (ctx->bL.cap < (size_t)bp * bp * 8 || ctx->bL_zeroed != (size_t)bp) {
-    HIPCHK(ensure(ctx->bL, (size_t)bp * bp * 8));
+    HIPCHK(ensure(ctx, ctx->bL, (size_t)bp * bp * 8));
     HIPCHK(hipMemsetAsync(ctx->bL.p, 0, (size_t)bp * bp * 8, s));
     ctx->bL_zeroed = (size_t)bp;
   }
-  HIPCHK(ensure(ctx->bPI, (size_t)bp * bp * 8));
-  HIPCHK(ensure(ctx->bH, (size_t)bp * bp * 8));
-  HIPCHK(ensure(ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(bp) * 8)));
-  HIPCHK(ensure(ctx->bvec, (size_t)(9 * bp + 3 * nfold + 8) * 8));
+  HIPCHK(ensure(ctx, ctx->bPI, (size_t)bp * bp * 8));
+  HIPCHK(ensure(ctx, ctx->bH, (size_t)bp * bp * 8));
+  HIPCHK(ensure(ctx, ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(bp) * 8)));
+  HIPCHK(ensure(ctx, ctx->bvec, (size_t)(9 * bp + 3 * nfold + 8) * 8));
   const int64_t nchunk = (bp + 255) / 256;
-  HIPCHK(ensure(ctx->slab, std::max(ctx->slab.cap, (size_t)nchunk * bp * 2 * 8)));
+  HIPCHK(ensure(ctx, ctx->slab, std::max(ctx->slab.cap, (size_t)nchunk * bp * 2 * 8)));
   double* v = ctx->bvec.d();
   double *ld = v, *af = v + bp, *t = v + 2 * bp, *r = v + 3 * bp, *c = v + 4 * bp,
          *gm = v + 5 * bp, *gc = v + 6 * bp, *w = v + 7 * bp, *yf = v + 8 * bp;
@@ -1018,8 +1072,8 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   const bool es_conc = esq && ctx->overlap && nfold > 1;
   double *PIs = nullptr, *RW = nullptr;
   if (es_conc) {
-    HIPCHK(ensure(ctx->bPIs, (size_t)nfold * bp * bp * 8));
-    HIPCHK(ensure(ctx->bRW, (size_t)2 * nfold * bp * 8));
+    HIPCHK(ensure(ctx, ctx->bPIs, (size_t)nfold * bp * bp * 8));
+    HIPCHK(ensure(ctx, ctx->bRW, (size_t)2 * nfold * bp * 8));
     PIs = ctx->bPIs.d();
     RW = ctx->bRW.d();
   }
@@ -1170,9 +1224,9 @@ int gps_ctx_create(int device, gps_ctx** out) {
   if (int rc = make_aux_streams(ctx)) return rc;
   HIPCHK(hipHostMalloc((void**)&ctx->hsmall, 256 * sizeof(double), hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&ctx->hinfo, 16, hipHostMallocDefault));
-  HIPCHK(ensure(ctx->info, 16));
-  HIPCHK(ensure(ctx->small, 256 * sizeof(double)));
-  HIPCHK(ensure(ctx->sk_cnt, (size_t)kStreamKTiles * sizeof(int)));
+  HIPCHK(ensure(ctx, ctx->info, 16));
+  HIPCHK(ensure(ctx, ctx->small, 256 * sizeof(double)));
+  HIPCHK(ensure(ctx, ctx->sk_cnt, (size_t)kStreamKTiles * sizeof(int)));
   HIPCHK(hipMemsetAsync(ctx->sk_cnt.p, 0, (size_t)kStreamKTiles * sizeof(int), ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   *out = ctx;
@@ -1188,15 +1242,16 @@ int gps_ctx_destroy(gps_ctx* ctx) {
     if (st) (void)hipStreamSynchronize(st);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   leave_local_group(ctx);
-  for (DBuf* b : ctx_buffers(ctx)) release(*b);
-  for (auto& kv : ctx->dag_lists) release(kv.second.first);
+  for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);  // before the buffers they use
+  ctx->pgraphs.clear();
+  for (DBuf* b : ctx_buffers(ctx)) release(ctx, *b);
+  for (auto& kv : ctx->dag_lists) release(ctx, kv.second.first);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->preb_fork, ctx->kn_fork, ctx->kn_join,
                        ctx->b_fork, ctx->b_join})
     if (e) (void)hipEventDestroy(e);
-  for (auto& g : ctx->pgraphs) (void)hipGraphExecDestroy(g.exec);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (hipStream_t l : ctx->aux)
     if (l) (void)hipStreamDestroy(l);
@@ -1234,11 +1289,16 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       if ((value != 0) == ctx->side_low) return 0;
       int least = 0, greatest = 0;
       HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      HIPCHK(hipStreamSynchronize(ctx->side));
-      HIPCHK(hipStreamDestroy(ctx->side));
-      ctx->side = nullptr;
-      if (value) HIPCHK(hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least));
-      else HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+      // the replacement first: if its creation fails, the context keeps its working side stream
+      // (never the legacy null stream, which would serialise against other contexts' captures)
+      hipStream_t ns = nullptr;
+      if (value) HIPCHK(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, least));
+      else HIPCHK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+      const hipError_t es = hipStreamSynchronize(ctx->side);
+      if (es != hipSuccess) (void)hipStreamDestroy(ns);
+      HIPCHK(es);
+      (void)hipStreamDestroy(ctx->side);
+      ctx->side = ns;
       ctx->side_low = value != 0;
       return 0;
     }
@@ -1284,6 +1344,8 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
   out[GPS_STAT_GRAPHS] = (int64_t)ctx->pgraphs.size();
   out[GPS_STAT_GRAPH_CAP] = (int64_t)kMaxGraphs;
   out[GPS_STAT_GRAPH_OVERFLOW] = ctx->graph_overflow;
+  out[GPS_STAT_GRAPH_DROPPED] = ctx->graph_dropped;
+  out[GPS_STAT_GRAPH_EVICTED] = ctx->graph_evicted;
   out[GPS_STAT_DEVICE_BYTES] = (int64_t)bytes;
   return 0;
 }
@@ -1350,7 +1412,7 @@ int gps_gram(gps_ctx* ctx, int kind, const double* X, int64_t n, const double* X
   const int64_t M = pad_to(n, 32), N = pad_to(m);
   if (int rc = upload(ctx, ctx->t0, X, n, d, n)) return rc;
   if (int rc = upload(ctx, ctx->t1, Xp, m, d, m)) return rc;
-  HIPCHK(ensure(ctx->t2, (size_t)M * N * 8));
+  HIPCHK(ensure(ctx, ctx->t2, (size_t)M * N * 8));
   HIPCHK(hipMemsetAsync(ctx->t2.p, 0, (size_t)M * N * 8, ctx->stream));
   if (int rc = gram(ctx, "gram_user", ctx->t0.d(), (int)n, ctx->t1.d(), (int)m, d, th, diag_add,
                     uplo == GPS_LOWER, 0, ctx->t2.d(), N, (int)M, (int)N))
@@ -1365,15 +1427,15 @@ int gps_gram(gps_ctx* ctx, int kind, const double* X, int64_t n, const double* X
 static int factor_user(gps_ctx* ctx, int64_t n, const double* A, int64_t lda, bool want_L) {
   ARGCHK(A && n > 0 && lda >= n, "bad matrix argument");
   const int64_t np = pad_to(n);
-  HIPCHK(ensure(ctx->t0, (size_t)n * lda * 8));
+  HIPCHK(ensure(ctx, ctx->t0, (size_t)n * lda * 8));
   HIPCHK(hipMemcpyAsync(ctx->t0.p, A, (size_t)n * lda * 8, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(ensure(ctx->t1, (size_t)np * np * 8));
+  HIPCHK(ensure(ctx, ctx->t1, (size_t)np * np * 8));
   HIPCHK(launch_pad_copy(ctx->t0.d(), lda, ctx->t1.d(), np, (int)n, (int)n, (int)np, (int)np, 1,
                          ctx->stream));
-  HIPCHK(ensure(ctx->t2, (size_t)np * np * 8));
+  HIPCHK(ensure(ctx, ctx->t2, (size_t)np * np * 8));
   HIPCHK(hipMemsetAsync(ctx->t2.p, 0, (size_t)np * np * 8, ctx->stream));  // L⁻¹ upper tiles = 0
-  HIPCHK(ensure(ctx->t3, potrf_ws_doubles(np) * 8));
-  HIPCHK(ensure(ctx->t4, (size_t)np * 8 * (want_L ? np + 1 : 1)));
+  HIPCHK(ensure(ctx, ctx->t3, potrf_ws_doubles(np) * 8));
+  HIPCHK(ensure(ctx, ctx->t4, (size_t)np * 8 * (want_L ? np + 1 : 1)));
   double* logdiag = ctx->t4.d();
   double* Lout = want_L ? ctx->t4.d() + np : nullptr;
   if (want_L) HIPCHK(hipMemsetAsync(Lout, 0, (size_t)np * np * 8, ctx->stream));
@@ -1403,11 +1465,11 @@ int gps_potrs(gps_ctx* ctx, int64_t n, int64_t nrhs, const double* A, int64_t ld
   if (int rc = factor_user(ctx, n, A, lda, false)) return rc;
   const int64_t np = pad_to(n), rp = pad_to(nrhs);
   // B padded into t0 (reuse), Y = L⁻¹B into t1, X = L⁻ᵀY into t3
-  HIPCHK(ensure(ctx->t0, (size_t)n * ldb * 8));
+  HIPCHK(ensure(ctx, ctx->t0, (size_t)n * ldb * 8));
   HIPCHK(hipMemcpyAsync(ctx->t0.p, B, (size_t)n * ldb * 8, hipMemcpyHostToDevice, ctx->stream));
   DBuf Bp, Y;
-  HIPCHK(ensure(Bp, (size_t)np * rp * 8));
-  HIPCHK(ensure(Y, (size_t)np * rp * 8));
+  HIPCHK(ensure(ctx, Bp, (size_t)np * rp * 8));
+  HIPCHK(ensure(ctx, Y, (size_t)np * rp * 8));
   int rc = 0;
   do {
     hipError_t e = launch_pad_copy(ctx->t0.d(), ldb, Bp.d(), rp, (int)n, (int)nrhs, (int)np,
@@ -1426,8 +1488,8 @@ int gps_potrs(gps_ctx* ctx, int64_t n, int64_t nrhs, const double* A, int64_t ld
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) rc = fail(ctx, -2, hipGetErrorString(e));
   } while (0);
-  release(Bp);
-  release(Y);
+  release(ctx, Bp);
+  release(ctx, Y);
   return rc;
 }
 
@@ -1437,7 +1499,7 @@ int gps_diag_inv(gps_ctx* ctx, int64_t n, const double* A, int64_t lda, double* 
   if (int rc = factor_user(ctx, n, A, lda, false)) return rc;
   const int64_t np = pad_to(n);
   const int64_t nchunk = (np + 255) / 256;
-  HIPCHK(ensure(ctx->t0, (size_t)(nchunk * np * 2 + np) * 8));
+  HIPCHK(ensure(ctx, ctx->t0, (size_t)(nchunk * np * 2 + np) * 8));
   double* out = ctx->t0.d() + nchunk * np * 2;
   HIPCHK(launch_colred(ctx->t2.d(), np, (int)np, (int)np, 1, nullptr, nullptr, nullptr, out,
                        ctx->t0.d(), ctx->stream));
@@ -1456,13 +1518,13 @@ int gps_gemm(gps_ctx* ctx, int transA, int transB, int64_t M, int64_t N, int64_t
   const int64_t ar = transA ? K : M, ac = transA ? M : K, arp = transA ? Kp : Mp, acp = transA ? Mp : Kp;
   const int64_t br = transB ? N : K, bc = transB ? K : N, brp = transB ? Np : Kp, bcp = transB ? Kp : Np;
   ARGCHK(lda >= ac && ldb >= bc && ldc >= N, "leading dimension too small");
-  HIPCHK(ensure(ctx->t0, (size_t)(ar * lda + br * ldb + M * ldc) * 8));
+  HIPCHK(ensure(ctx, ctx->t0, (size_t)(ar * lda + br * ldb + M * ldc) * 8));
   double* rawA = ctx->t0.d();
   double* rawB = rawA + ar * lda;
   double* rawC = rawB + br * ldb;
   HIPCHK(hipMemcpyAsync(rawA, A, (size_t)ar * lda * 8, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(rawB, B, (size_t)br * ldb * 8, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(ensure(ctx->t1, (size_t)(arp * acp + brp * bcp + Mp * Np) * 8));
+  HIPCHK(ensure(ctx, ctx->t1, (size_t)(arp * acp + brp * bcp + Mp * Np) * 8));
   double* pA = ctx->t1.d();
   double* pB = pA + arp * acp;
   double* pC = pB + brp * bcp;
@@ -1484,7 +1546,7 @@ int gps_gemm(gps_ctx* ctx, int transA, int transB, int64_t M, int64_t N, int64_t
 
 // scratch for the row finalisers' per-workgroup partials (kernels_vec.hip): nv per 256 rows
 static double* row_part(gps_ctx* ctx, int64_t rows, int nv) {
-  if (ensure(ctx->rpart, (size_t)(std::max<int64_t>(rows, 1) + 255) / 256 * nv * 8) != hipSuccess)
+  if (ensure(ctx, ctx->rpart, (size_t)(std::max<int64_t>(rows, 1) + 255) / 256 * nv * 8) != hipSuccess)
     return nullptr;
   return ctx->rpart.d();
 }
@@ -1552,21 +1614,21 @@ int full_fit_core(gps_ctx* ctx, int kind, const double* theta, int n_ell) {
   ctx->n_ell = n_ell;
   const int64_t n = ctx->n, np = ctx->n_pad;
   hipStream_t s = ctx->stream;
-  HIPCHK(ensure(ctx->A, (size_t)np * np * 8));
+  HIPCHK(ensure(ctx, ctx->A, (size_t)np * np * 8));
   if (ctx->Linv.cap < (size_t)np * np * 8 || ctx->linv_zeroed != (size_t)np) {
-    HIPCHK(ensure(ctx->Linv, (size_t)np * np * 8));
+    HIPCHK(ensure(ctx, ctx->Linv, (size_t)np * np * 8));
     HIPCHK(hipMemsetAsync(ctx->Linv.p, 0, (size_t)np * np * 8, s));
     ctx->linv_zeroed = (size_t)np;
   }
-  HIPCHK(ensure(ctx->W, potrf_ws_doubles(np) * 8));
-  HIPCHK(ensure(ctx->logdiag, np * 8));
-  HIPCHK(ensure(ctx->beta, np * 8));
-  HIPCHK(ensure(ctx->alpha, np * 8));
-  HIPCHK(ensure(ctx->dinv, np * 8));
-  HIPCHK(ensure(ctx->mu_loo, np * 8));
-  HIPCHK(ensure(ctx->var_loo, np * 8));
+  HIPCHK(ensure(ctx, ctx->W, potrf_ws_doubles(np) * 8));
+  HIPCHK(ensure(ctx, ctx->logdiag, np * 8));
+  HIPCHK(ensure(ctx, ctx->beta, np * 8));
+  HIPCHK(ensure(ctx, ctx->alpha, np * 8));
+  HIPCHK(ensure(ctx, ctx->dinv, np * 8));
+  HIPCHK(ensure(ctx, ctx->mu_loo, np * 8));
+  HIPCHK(ensure(ctx, ctx->var_loo, np * 8));
   const int64_t nchunk = (np + 255) / 256;
-  HIPCHK(ensure(ctx->slab, (size_t)nchunk * np * 2 * 8));
+  HIPCHK(ensure(ctx, ctx->slab, (size_t)nchunk * np * 2 * 8));
   int rc;
   if ((rc = reset_info(ctx))) return rc;
   if ((rc = gram(ctx, "gram_kff", ctx->X.d(), (int)n, ctx->X.d(), (int)n, ctx->d, ctx->th,
@@ -1649,10 +1711,10 @@ int gps_full_grad(gps_ctx* ctx, int kind, const double* theta, int n_ell, int ob
     g.a0 = 0.5;
     g.a1 = -0.5;
   } else {
-    HIPCHK(ensure(ctx->gu, np * 8));
-    HIPCHK(ensure(ctx->gct, np * 8));
-    HIPCHK(ensure(ctx->gv, np * 8));
-    HIPCHK(ensure(ctx->Mx, (size_t)np * np * 8));
+    HIPCHK(ensure(ctx, ctx->gu, np * 8));
+    HIPCHK(ensure(ctx, ctx->gct, np * 8));
+    HIPCHK(ensure(ctx, ctx->gv, np * 8));
+    HIPCHK(ensure(ctx, ctx->Mx, (size_t)np * np * 8));
     {
       Prof pr(ctx, "grad_mirror", 0, 16.0 * (double)np * np / 2);
       HIPCHK(launch_sym_mirror(ctx->A.d(), np, (int)np, s));
@@ -1676,8 +1738,8 @@ int gps_full_grad(gps_ctx* ctx, int kind, const double* theta, int n_ell, int ob
     g.Mx = ctx->Mx.d();
   }
   const int passes = grad_contract_passes(d);
-  HIPCHK(ensure(ctx->gslab, (size_t)grad_contract_slab_doubles((int)n, d) * 8));
-  HIPCHK(ensure(ctx->gout, (size_t)passes * 18 * 8));
+  HIPCHK(ensure(ctx, ctx->gslab, (size_t)grad_contract_slab_doubles((int)n, d) * 8));
+  HIPCHK(ensure(ctx, ctx->gout, (size_t)passes * 18 * 8));
   g.slab = ctx->gslab.d();
   {
     Prof pr(ctx, "grad_contract", 0, (objective == GPS_OBJ_NLML ? 8.0 : 16.0) * (double)n * n / 2);
@@ -1711,13 +1773,13 @@ int gps_full_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   const int64_t n = ctx->n, np = ctx->n_pad, nt = ctx->nt, ntp = ctx->nt_pad;
   hipStream_t s = ctx->stream;
   const int64_t tiles_m = np / GPS_TILE;
-  HIPCHK(ensure(ctx->s1, ntp * 8));
-  HIPCHK(ensure(ctx->s2, ntp * 8));
-  HIPCHK(ensure(ctx->mu, ntp * 8));
-  HIPCHK(ensure(ctx->var, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->s1, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->s2, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->mu, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->var, ntp * 8));
   int rc;
-  HIPCHK(ensure(ctx->Ksf, (size_t)ntp * np * 8));
-  HIPCHK(ensure(ctx->pslab, (size_t)tiles_m * ntp * 2 * 8));
+  HIPCHK(ensure(ctx, ctx->Ksf, (size_t)ntp * np * 8));
+  HIPCHK(ensure(ctx, ctx->pslab, (size_t)tiles_m * ntp * 2 * 8));
   if ((rc = gram(ctx, "gram_ksf", ctx->Xt.d(), (int)nt, ctx->X.d(), (int)n, ctx->d, ctx->th, 0.0, 0,
                  0, ctx->Ksf.d(), np, (int)ntp, (int)np)))
     return rc;
@@ -1850,7 +1912,7 @@ int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* ds
               bool packed = false) {
   const int64_t mp = ctx->m_pad;
   const int ks = fitc_syrk_ks(ctx);
-  HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->slabB, (size_t)ks * mp * mp * 8));
   GemmParams p = gp0();
   p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
   p.C = ctx->slabB.d(); p.ldc = mp; p.c_kslice_stride = mp * mp;
@@ -1881,7 +1943,7 @@ int fitc_syrk_allreduce(gps_ctx* ctx, double* red, int64_t blen, int64_t tail) {
     return allreduce_sum(ctx, red, (size_t)(blen + tail), s);
   }
   const int ks = fitc_syrk_ks(ctx);
-  HIPCHK(ensure(ctx->slabB, (size_t)ks * mp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->slabB, (size_t)ks * mp * mp * 8));
   hipStream_t cs = ctx->aux[1];
   while ((int)ctx->ar_ev.size() < nch + 1) {
     hipEvent_t e;
@@ -1923,9 +1985,9 @@ int fitc_test_prepass(gps_ctx* ctx) {
   const int64_t nt = ctx->fnt, ntp = ctx->fnt_pad, m = ctx->m, mp = ctx->m_pad;
   const int64_t tm = mp / GPS_TILE;
   hipStream_t a = ctx->aux[0];
-  HIPCHK(ensure(ctx->Ksm, (size_t)ntp * mp * 8));
-  HIPCHK(ensure(ctx->qm, ntp * 8));
-  HIPCHK(ensure(ctx->fslab_pre, (size_t)tm * ntp * 8));
+  HIPCHK(ensure(ctx, ctx->Ksm, (size_t)ntp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->qm, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->fslab_pre, (size_t)tm * ntp * 8));
   for (hipEvent_t* e : {&ctx->pre_fork, &ctx->pre_join})
     if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   HIPCHK(hipEventRecord(ctx->pre_fork, ctx->stream));
@@ -1951,7 +2013,7 @@ int fitc_test_prepass(gps_ctx* ctx) {
 int fitc_test_prepass_b(gps_ctx* ctx) {
   const int64_t ntp = ctx->fnt_pad, mp = ctx->m_pad, tm = mp / GPS_TILE;
   hipStream_t a = ctx->aux[0];
-  HIPCHK(ensure(ctx->qb, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->qb, ntp * 8));
   if (!ctx->preb_fork) HIPCHK(hipEventCreateWithFlags(&ctx->preb_fork, hipEventDisableTiming));
   HIPCHK(hipEventRecord(ctx->preb_fork, ctx->stream));
   HIPCHK(hipStreamWaitEvent(a, ctx->preb_fork, 0));
@@ -1979,42 +2041,42 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   const int64_t tm = mp / GPS_TILE;
   hipStream_t s = ctx->stream;
   // buffers
-  HIPCHK(ensure(ctx->Kmm, (size_t)mp * mp * 8));
-  HIPCHK(ensure(ctx->Am, (size_t)mp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->Kmm, (size_t)mp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->Am, (size_t)mp * mp * 8));
   if (ctx->lm_zeroed != (size_t)mp || ctx->Lm.cap < (size_t)mp * mp * 8) {
-    HIPCHK(ensure(ctx->Lm, (size_t)mp * mp * 8));
-    HIPCHK(ensure(ctx->Lb, (size_t)mp * mp * 8));
+    HIPCHK(ensure(ctx, ctx->Lm, (size_t)mp * mp * 8));
+    HIPCHK(ensure(ctx, ctx->Lb, (size_t)mp * mp * 8));
     HIPCHK(hipMemsetAsync(ctx->Lm.p, 0, (size_t)mp * mp * 8, s));
     HIPCHK(hipMemsetAsync(ctx->Lb.p, 0, (size_t)mp * mp * 8, s));
     ctx->lm_zeroed = (size_t)mp;
   }
-  HIPCHK(ensure(ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(mp) * 8)));
-  HIPCHK(ensure(ctx->ldm, mp * 8));
-  HIPCHK(ensure(ctx->ldb, mp * 8));
-  HIPCHK(ensure(ctx->Knm, (size_t)np * mp * 8));
-  HIPCHK(ensure(ctx->q, np * 8));
-  HIPCHK(ensure(ctx->lam, np * 8));
-  HIPCHK(ensure(ctx->ilam, np * 8));
-  HIPCHK(ensure(ctx->ys, np * 8));
-  HIPCHK(ensure(ctx->r, np * 8));
-  HIPCHK(ensure(ctx->g, np * 8));
-  HIPCHK(ensure(ctx->fmu_loo, np * 8));
-  HIPCHK(ensure(ctx->fvar_loo, np * 8));
-  HIPCHK(ensure(ctx->c, mp * 8));
-  HIPCHK(ensure(ctx->tvec, mp * 8));
+  HIPCHK(ensure(ctx, ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(mp) * 8)));
+  HIPCHK(ensure(ctx, ctx->ldm, mp * 8));
+  HIPCHK(ensure(ctx, ctx->ldb, mp * 8));
+  HIPCHK(ensure(ctx, ctx->Knm, (size_t)np * mp * 8));
+  HIPCHK(ensure(ctx, ctx->q, np * 8));
+  HIPCHK(ensure(ctx, ctx->lam, np * 8));
+  HIPCHK(ensure(ctx, ctx->ilam, np * 8));
+  HIPCHK(ensure(ctx, ctx->ys, np * 8));
+  HIPCHK(ensure(ctx, ctx->r, np * 8));
+  HIPCHK(ensure(ctx, ctx->g, np * 8));
+  HIPCHK(ensure(ctx, ctx->fmu_loo, np * 8));
+  HIPCHK(ensure(ctx, ctx->fvar_loo, np * 8));
+  HIPCHK(ensure(ctx, ctx->c, mp * 8));
+  HIPCHK(ensure(ctx, ctx->tvec, mp * 8));
   // all-reduce buffer [B | b | scalars]: B lower-packed (m(m+1)/2) when the rows are sharded,
   // the padded lower tiles (m_pad²) on one rank
   const bool shard = sharded(ctx);
   const int64_t blen = shard ? m * (m + 1) / 2 : mp * mp;
   const int64_t red_len = mp * mp + mp + 8;
-  HIPCHK(ensure(ctx->red, (size_t)red_len * 8));
+  HIPCHK(ensure(ctx, ctx->red, (size_t)red_len * 8));
   const int64_t nchunk = (std::max(np, mp) + 255) / 256;
   // (row-norm partials tm·np; column passes' chunk partials: Knm's 256-row chunks, and, after
   //  the r pass's first column tiles (formed during B's factorisation), the m×m pass for c in
   //  32-row chunks)
   const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * np, nchunk * mp * 2),
                                               tm * np + (mp + 31) / 32 * mp);
-  HIPCHK(ensure(ctx->fslab, (size_t)fslab_len * 8));
+  HIPCHK(ensure(ctx, ctx->fslab, (size_t)fslab_len * 8));
   double* red = ctx->red.d();
   double* Bacc = red;
   double* bvec = red + blen;
@@ -2194,17 +2256,17 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   const bool loo = objective != GPS_OBJ_NLML;
   const double a = loo ? 0.0 : 0.5;
   // scratch
-  HIPCHK(ensure(ctx->fgv, (size_t)11 * np * 8));
-  HIPCHK(ensure(ctx->fgm, (size_t)6 * mp * 8));
+  HIPCHK(ensure(ctx, ctx->fgv, (size_t)11 * np * 8));
+  HIPCHK(ensure(ctx, ctx->fgm, (size_t)6 * mp * 8));
   const bool shard = sharded(ctx);
-  HIPCHK(ensure(ctx->fgB, (size_t)(shard ? 6 : 5) * mp * mp * 8));
-  HIPCHK(ensure(ctx->fR, (size_t)np * 3 * mp * 8));
-  HIPCHK(ensure(ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
+  HIPCHK(ensure(ctx, ctx->fgB, (size_t)(shard ? 6 : 5) * mp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->fR, (size_t)np * 3 * mp * 8));
+  HIPCHK(ensure(ctx, ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
   const int passes = fitc_contract_passes(d);
   const int64_t outlen = (int64_t)passes * 17 + m * d;
-  HIPCHK(ensure(ctx->fgslab, (size_t)std::max(fitc_contract_slab_doubles((int)n, (int)mp, d),
+  HIPCHK(ensure(ctx, ctx->fgslab, (size_t)std::max(fitc_contract_slab_doubles((int)n, (int)mp, d),
                                                fitc_contract_slab_doubles((int)m, (int)mp, d)) * 8));
-  HIPCHK(ensure(ctx->fgout, (size_t)(2 * outlen + 8) * 8));
+  HIPCHK(ensure(ctx, ctx->fgout, (size_t)(2 * outlen + 8) * 8));
   double* vbase = ctx->fgv.d();
   double *alpha = vbase, *dinv = vbase + np, *v = vbase + 2 * np, *ulam = vbase + 3 * np,
          *h = vbase + 4 * np, *hl2 = vbase + 5 * np, *md = vbase + 6 * np, *s1 = vbase + 7 * np,
@@ -2379,9 +2441,9 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
   };
   double* Gblk = nullptr;
   if (grad) {  // zero outside the fold squares (which move with n and nfold): cleared per call
-    HIPCHK(ensure(ctx->bGblk, (size_t)np * np * 8));
+    HIPCHK(ensure(ctx, ctx->bGblk, (size_t)np * np * 8));
     HIPCHK(hipMemsetAsync(ctx->bGblk.p, 0, (size_t)np * np * 8, s));
-    HIPCHK(ensure(ctx->gu, np * 8));
+    HIPCHK(ensure(ctx, ctx->gu, np * 8));
     HIPCHK(hipMemsetAsync(ctx->gu.p, 0, np * 8, s));
     Gblk = ctx->bGblk.d();
   }
@@ -2400,9 +2462,9 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
     for (int f = 0; f < nfold; ++f) fold_values[f] = fv[f];
   if (!grad) return 0;
   const int d = ctx->d;
-  HIPCHK(ensure(ctx->gv, np * 8));
-  HIPCHK(ensure(ctx->Mx, (size_t)np * np * 8));
-  HIPCHK(ensure(ctx->bT, (size_t)np * np * 8));
+  HIPCHK(ensure(ctx, ctx->gv, np * 8));
+  HIPCHK(ensure(ctx, ctx->Mx, (size_t)np * np * 8));
+  HIPCHK(ensure(ctx, ctx->bT, (size_t)np * np * 8));
   HIPCHK(launch_gemv_full(Ainv, np, ctx->gu.d(), ctx->gv.d(), (int)np, (int)np, s));
   {  // T = A⁻¹ Gblk, K restricted per 16-column group to the folds those columns touch
     const std::vector<int64_t> bnd = fold_bounds(n, nfold);
@@ -2423,7 +2485,7 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
       kr[2 * q] = (int)(bnd[fold_of(c0)] / 16 * 16);
       kr[2 * q + 1] = (int)std::min<int64_t>(np, (bnd[fold_of(c1) + 1] + 15) / 16 * 16);
     }
-    HIPCHK(ensure(ctx->bkr, kr.size() * sizeof(int)));
+    HIPCHK(ensure(ctx, ctx->bkr, kr.size() * sizeof(int)));
     HIPCHK(hipMemcpyAsync(ctx->bkr.p, kr.data(), kr.size() * sizeof(int), hipMemcpyHostToDevice, s));
     GemmParams p = gp0();
     p.A = Ainv; p.lda = np; p.B = Gblk; p.ldb = np; p.C = ctx->bT.d(); p.ldc = np;
@@ -2445,8 +2507,8 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
   gpar.Ainv = Ainv; gpar.ldm = np; gpar.alpha = ctx->alpha.d();
   gpar.a2 = -1.0; gpar.a3 = -1.0; gpar.v = ctx->gv.d(); gpar.Mx = ctx->Mx.d();
   const int passes = grad_contract_passes(d);
-  HIPCHK(ensure(ctx->gslab, (size_t)grad_contract_slab_doubles((int)n, d) * 8));
-  HIPCHK(ensure(ctx->gout, (size_t)passes * 18 * 8));
+  HIPCHK(ensure(ctx, ctx->gslab, (size_t)grad_contract_slab_doubles((int)n, d) * 8));
+  HIPCHK(ensure(ctx, ctx->gout, (size_t)passes * 18 * 8));
   gpar.slab = ctx->gslab.d();
   {
     Prof pr(ctx, "grad_contract", 0, 16.0 * (double)n * n / 2);
@@ -2493,7 +2555,7 @@ int gps_full_blockloo_es(gps_ctx* ctx, int kind, const double* theta, int n_ell,
   ARGCHK(ctx->have_data, "gps_full_set_data first");
   ARGCHK(n_ell == 1 || n_ell == ctx->d, "n_ell must be 1 or d");
   const int64_t cnt = 2 * (int64_t)num_sim * ctx->n;
-  HIPCHK(ensure(ctx->edraws, (size_t)cnt * 8));
+  HIPCHK(ensure(ctx, ctx->edraws, (size_t)cnt * 8));
   HIPCHK(hipMemcpyAsync(ctx->edraws.p, draws, (size_t)cnt * 8, hipMemcpyHostToDevice, ctx->stream));
   EsArgs es;
   es.S = num_sim;
@@ -2517,7 +2579,7 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
   hipStream_t s = ctx->stream;
   const int64_t bp = pad_to(b);
   if (int rc = upload(ctx, ctx->t0, C, b, b, b)) return rc;
-  HIPCHK(ensure(ctx->bPI, (size_t)bp * bp * 8));
+  HIPCHK(ensure(ctx, ctx->bPI, (size_t)bp * bp * 8));
   HIPCHK(launch_pad_copy(ctx->t0.d(), b, ctx->bPI.d(), bp, (int)b, (int)b, (int)bp, (int)bp, 1, s));
   std::vector<double> r(b);  // the residual y − m (input marshalling: ẑ_S = m − y = −r)
   double tr = 0.0;
@@ -2527,9 +2589,9 @@ int gps_energy_score(gps_ctx* ctx, const double* m, const double* C, int64_t b, 
   }
   ARGCHK(tr > 0.0, "C must be positive definite");
   if (int rc = upload(ctx, ctx->t1, r.data(), b, 1, bp)) return rc;
-  HIPCHK(ensure(ctx->t2, (size_t)bp * 8));
+  HIPCHK(ensure(ctx, ctx->t2, (size_t)bp * 8));
   const int64_t cnt = 2 * (int64_t)num_sim * b;
-  HIPCHK(ensure(ctx->edraws, (size_t)cnt * 8));
+  HIPCHK(ensure(ctx, ctx->edraws, (size_t)cnt * 8));
   HIPCHK(hipMemcpyAsync(ctx->edraws.p, draws, (size_t)cnt * 8, hipMemcpyHostToDevice, s));
   EsArgs es;
   es.S = num_sim;
@@ -2561,7 +2623,7 @@ static int local_folds(gps_ctx* ctx, int nfold, std::vector<int64_t>& bnd, std::
   }
   const int P = ctx->nranks;
   hipStream_t s = ctx->stream;
-  HIPCHK(ensure(ctx->bfv, (size_t)std::max(P, 64) * 8));
+  HIPCHK(ensure(ctx, ctx->bfv, (size_t)std::max(P, 64) * 8));
   std::vector<double> cnt((size_t)P, 0.0);
   cnt[ctx->rank] = (double)n;
   HIPCHK(hipMemcpyAsync(ctx->bfv.p, cnt.data(), (size_t)P * 8, hipMemcpyHostToDevice, s));
@@ -2626,8 +2688,8 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   const bool want = grad != nullptr || grad_z != nullptr;
   const int64_t ldr = want ? 3 * mp : mp;  // [U | E | K Km⁻¹]; U's slot later holds KS, KB⁻¹T
   const int64_t bp = bounds_pad(bnd);
-  HIPCHK(ensure(ctx->fR, (size_t)np * ldr * 8));
-  HIPCHK(ensure(ctx->fgv, (size_t)13 * np * 8));
+  HIPCHK(ensure(ctx, ctx->fR, (size_t)np * ldr * 8));
+  HIPCHK(ensure(ctx, ctx->fgv, (size_t)13 * np * 8));
   double* U = ctx->fR.d();
   double* E = U + mp;
   double* RC = U + 2 * mp;
@@ -2654,7 +2716,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   double *Binv = nullptr, *Kminv = nullptr, *Sm = nullptr, *Tm = nullptr, *BT = nullptr,
          *KmD = nullptr, *F = nullptr;
   if (want) {
-    HIPCHK(ensure(ctx->fgB, (size_t)(shard ? 7 : 6) * mp * mp * 8));
+    HIPCHK(ensure(ctx, ctx->fgB, (size_t)(shard ? 7 : 6) * mp * mp * 8));
     double* Bb = ctx->fgB.d();
     Binv = Bb; Kminv = Bb + mp * mp; Sm = Bb + 2 * mp * mp; Tm = Bb + 3 * mp * mp;
     BT = Bb + 4 * mp * mp; KmD = Bb + 5 * mp * mp;
@@ -2669,16 +2731,16 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     }
     if ((rc = gemm_nn(ctx->Knm.d(), mp, Binv, E, ldr, np))) return rc;  // E = Λ⁻¹ K B⁻¹
     HIPCHK(launch_row_scale(E, ldr, (int)np, (int)mp, ctx->ilam.d(), s));
-    HIPCHK(ensure(ctx->bF, (size_t)np * mp * 8));
-    HIPCHK(ensure(ctx->bEf, (size_t)bp * mp * 8));
-    HIPCHK(ensure(ctx->bFf, (size_t)bp * mp * 8));
-    HIPCHK(ensure(ctx->bG, (size_t)bp * bp * 8));
+    HIPCHK(ensure(ctx, ctx->bF, (size_t)np * mp * 8));
+    HIPCHK(ensure(ctx, ctx->bEf, (size_t)bp * mp * 8));
+    HIPCHK(ensure(ctx, ctx->bFf, (size_t)bp * mp * 8));
+    HIPCHK(ensure(ctx, ctx->bG, (size_t)bp * bp * 8));
     HIPCHK(hipMemsetAsync(ctx->bG.p, 0, (size_t)bp * bp * 8, s));
     F = ctx->bF.d();
     HIPCHK(hipMemsetAsync(F, 0, (size_t)np * mp * 8, s));
     HIPCHK(hipMemsetAsync(gg, 0, (size_t)2 * np * 8, s));  // g and diag(Gblk)
   }
-  HIPCHK(ensure(ctx->bT, (size_t)bp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->bT, (size_t)bp * mp * 8));
   auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bpp) -> int {
     double* Uf = ctx->bT.d();
     HIPCHK(launch_pad_copy(U + a * ldr, ldr, Uf, mp, (int)b, (int)mp, (int)bpp, (int)mp, 0, s));
@@ -2720,7 +2782,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     for (int f = 0; f < nfold; ++f) fold_values[f] = fv[f];
   if (!want) return 0;
   // v = C⁻¹g = g/λ − Λ⁻¹K B⁻¹Kᵀ(g/λ)
-  HIPCHK(ensure(ctx->fgm, (size_t)6 * mp * 8));
+  HIPCHK(ensure(ctx, ctx->fgm, (size_t)6 * mp * 8));
   double* mb = ctx->fgm.d();
   double *tku = mb, *tbt = mb + mp, *what = mb + 2 * mp;
   HIPCHK(launch_vec_mul(gg, ctx->ilam.d(), (int)np, ulam, s));
@@ -2753,7 +2815,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   // ŵ = Km⁻¹Kᵀv;  Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹;  Σ M_ii
   // [P | Σ M_ii | (pad) | Kᵀv]: P = Kᵀdiag(M_ii)K lower-packed (m(m+1)/2) when sharded, else
   // the padded lower tiles (gps_fitc_grad's layout)
-  HIPCHK(ensure(ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
+  HIPCHK(ensure(ctx, ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
   const int64_t plen = shard ? m * (m + 1) / 2 : mp * mp;
   const int64_t off_tw = (plen + 2) / 2 * 2;
   double* red = ctx->fgred.d();
@@ -2778,9 +2840,9 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   // contractions with ∂Knm/∂θ, ∂Knm/∂Z and ∂Kmm/∂θ, ∂Kmm/∂Z
   const int passes = fitc_contract_passes(d);
   const int64_t outlen = (int64_t)passes * 17 + m * d;
-  HIPCHK(ensure(ctx->fgslab, (size_t)std::max(fitc_contract_slab_doubles((int)n, (int)mp, d),
+  HIPCHK(ensure(ctx, ctx->fgslab, (size_t)std::max(fitc_contract_slab_doubles((int)n, (int)mp, d),
                                                fitc_contract_slab_doubles((int)m, (int)mp, d)) * 8));
-  HIPCHK(ensure(ctx->fgout, (size_t)(2 * outlen + 8) * 8));
+  HIPCHK(ensure(ctx, ctx->fgout, (size_t)(2 * outlen + 8) * 8));
   double* out1 = ctx->fgout.d();
   double* out2 = out1 + outlen;
   FitcContractParams cp;
@@ -2850,12 +2912,12 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
   const int64_t nt = ctx->fnt, ntp = ctx->fnt_pad, m = ctx->m, mp = ctx->m_pad;
   const int64_t tm = mp / GPS_TILE;
   hipStream_t s = ctx->stream;
-  HIPCHK(ensure(ctx->Ksm, (size_t)ntp * mp * 8));
-  HIPCHK(ensure(ctx->qm, ntp * 8));
-  HIPCHK(ensure(ctx->qb, ntp * 8));
-  HIPCHK(ensure(ctx->fmu, ntp * 8));
-  HIPCHK(ensure(ctx->fvar, ntp * 8));
-  HIPCHK(ensure(ctx->fslab, std::max(ctx->fslab.cap, (size_t)tm * ntp * 8)));
+  HIPCHK(ensure(ctx, ctx->Ksm, (size_t)ntp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->qm, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->qb, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->fmu, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->fvar, ntp * 8));
+  HIPCHK(ensure(ctx, ctx->fslab, std::max(ctx->fslab.cap, (size_t)tm * ntp * 8)));
   double* sums = ctx->small.d() + 8;
   int rc;
   const bool pre = ctx->f_pre;  // K*m and q* came with the fit (fitc_test_prepass)
@@ -2954,7 +3016,7 @@ int gps_full_surface(gps_ctx* ctx, const double* X, const double* y, int64_t n, 
   if (int rc = upload(ctx, ctx->t2, ell, n_ell, 1, n_ell)) return rc;
   if (int rc = upload(ctx, ctx->t3, noise_sd, n_noise, 1, n_noise)) return rc;
   const int64_t cnt = 4 * n_ell * n_noise;
-  HIPCHK(ensure(ctx->t4, (size_t)cnt * 8));
+  HIPCHK(ensure(ctx, ctx->t4, (size_t)cnt * 8));
   SurfaceParams p;
   p.x = ctx->t0.d(); p.y = ctx->t1.d(); p.n = (int)n; p.d = d; p.sf2 = std::exp(log_sf2);
   p.ell = ctx->t2.d(); p.nl = (int)n_ell; p.sd = ctx->t3.d(); p.ns = (int)n_noise;

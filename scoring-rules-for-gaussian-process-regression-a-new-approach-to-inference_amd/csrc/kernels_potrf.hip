@@ -597,6 +597,7 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   int* out = nullptr;
   int* out2 = nullptr;
   unsigned long long* trow = nullptr;  // TRACE: the current slot's record
+  int ndone = 0;                       // queue slots this workgroup completed
   for (;;) {
     if (tid == 0) {
       if constexpr (TRACE) {  // (the previous task's "done" stamp lives here for the same reason)
@@ -653,13 +654,24 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
       }
       if (!c1) { c1 = c0; v1 = v0; }
       if (!c2) { c2 = c0; v2 = v0; }
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      unsigned int ab = 0;
+      // A lost dependency is declared only after spin_ticks of wall clock with no movement of
+      // the polled counts AND at least kMinPolls polls: time this queue spends descheduled (the
+      // GPU time-sliced to another process) advances the clock but not the poll count.
+      constexpr unsigned int kMinPolls = 100000;
+      unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned int ab = 0, polls = 0;
+      int seen = -1;
       for (;;) {
         const int a0 = ld_cnt(c0), a1 = ld_cnt(c1), a2 = ld_cnt(c2), e = ld_cnt(err);
         if (__builtin_amdgcn_readfirstlane((a0 >= v0 && a1 >= v1 && a2 >= v2) ? 1 : 0)) break;
         if (__builtin_amdgcn_readfirstlane(e != 0x7f7f7f7f ? 1 : 0)) { ab = 1; break; }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > p.spin_ticks) {  // a lost dependency
+        const int s = __builtin_amdgcn_readfirstlane(a0 + a1 + a2);
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if (s != seen) {  // progress: restart the clock
+          seen = s;
+          t0 = now;
+          polls = 0;
+        } else if (++polls > kMinPolls && now - t0 > p.spin_ticks) {
           if (tid == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ab = 1;
           break;
@@ -667,7 +679,11 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
         __builtin_amdgcn_s_sleep(2);
       }
       if (tid == 0) sh[1] = ab;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no loads above the poll
+      // agent-scope acquire: the producers' payload (stored write-through, drained, then the
+      // relaxed agent-scope arrival) is visible to every load after this fence by the memory
+      // model itself — the other waves are ordered behind it by the workgroup barrier below —
+      // not only by the sc1 loads happening to miss the CU cache.
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(sh[1])) break;
@@ -736,10 +752,14 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
     //      the first thing lane 0 does at the top of the next iteration
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    ++ndone;
   }
   // ---- the last workgroup out zeroes this launch's counters for the next launch (no memset node
-  //      ahead of a replayed sequence).  Every workgroup first waits for its own counter atomics
-  //      (the last arrival has no return value; vmcnt covers it), then counts itself out.
+  //      ahead of a replayed sequence).  Every workgroup first adds the tasks it completed to
+  //      cnt[2] and waits for its own counter atomics (the last arrival and that add have no
+  //      return value; vmcnt covers them), then counts itself out.
+  if (tid == 0 && ndone)
+    __hip_atomic_fetch_add(p.cnt + 2, ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -748,6 +768,18 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   }
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(sh[1])) {
+    // The run is complete only if every queue slot was executed once and each workgroup fetched
+    // exactly one slot past the end: counters that were not zero at launch (the round-3 "no-op
+    // replay": a head counter >= ntasks makes every workgroup leave at once and Linv / logdiag
+    // unwritten) are reported as error 2 instead of passing check_info silently.
+    if (tid == 0) {
+      const int head_end = __hip_atomic_load(p.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int done = __hip_atomic_load(p.cnt + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (e == 0x7f7f7f7f && (done != p.ntasks || head_end != p.ntasks + (int)gridDim.x))
+        __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
     const int n = 16 + 2 * T * T;
     for (int i = tid; i < n; i += 256)
       __hip_atomic_store(p.cnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -218,12 +218,13 @@ class Context:
         self.call("gps_ctx_synchronize")
 
     def stats(self):
-        """{graphs, graph_cap, graph_overflow, device_bytes} (gps_ctx_stats)."""
+        """{graphs, graph_cap, graph_overflow, device_bytes, graph_dropped, graph_evicted}
+        (gps_ctx_stats)."""
         import numpy as np
-        out = np.zeros(4, np.int64)
+        out = np.zeros(6, np.int64)
         self.call("gps_ctx_stats", out.ctypes.data_as(ctypes.c_void_p))
-        return dict(zip(("graphs", "graph_cap", "graph_overflow", "device_bytes"),
-                        (int(v) for v in out)))
+        return dict(zip(("graphs", "graph_cap", "graph_overflow", "device_bytes", "graph_dropped",
+                         "graph_evicted"), (int(v) for v in out)))
 
     def set_stream(self, stream_handle):
         self.call("gps_ctx_set_stream", _c_vp(stream_handle))

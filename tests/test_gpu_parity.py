@@ -640,7 +640,7 @@ def test_ctx_stats_graph_cache(gpu_ctx):
     s1 = gpu_ctx.stats()
     gp.fit(theta=(0.1, 0.0, np.log(0.01)))
     s2 = gpu_ctx.stats()
-    assert s1["graph_cap"] == 256 and 1 <= s1["graphs"] <= s1["graph_cap"]
+    assert s1["graph_cap"] == 64 and 1 <= s1["graphs"] <= s1["graph_cap"]
     assert s2["graphs"] == s1["graphs"] and s2["graph_overflow"] == s1["graph_overflow"]
     assert s1["device_bytes"] > 700 * 700 * 8
 

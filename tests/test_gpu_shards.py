@@ -149,6 +149,22 @@ def test_fitc_shards_large_m(gpu_ctx):
              "fitc_shards_large_m")
 
 
+def test_c5_sharded_p8(gpu_ctx):
+    """BASELINE.json configs[4] in its stated form: C5 (FITC n = 200 000, m = 4000, d = 16,
+    n* = 10 000, the bench's own inputs) with the rows split 8 ways — 8 shard contexts on device 0
+    joined by the in-process communicator, B's all-reduce in 4 row blocks (the default) — against
+    the unsharded N = 1 unit: every objective, the concatenated LOO / predictive vectors and the
+    global test scores within 30× the measured floor and under fitc_cap (K20:222-234, 270-296)."""
+    from test_gpu_parity import _bench_inputs, fitc_cap
+    X, y, Xt, yt, Z, th = _bench_inputs("C5")
+    ref = _whole(X, y, Xt, yt, Z, th, False, gpu_ctx)
+    parts = _sharded(8, X, y, Xt, yt, Z, th, False)
+    assert sum(len(p["mu_loo"]) for p in parts) == len(y)
+    assert sum(len(p["mu"]) for p in parts) == len(yt)
+    _compare(parts, ref, _floor(X, y, Xt, yt, Z, th, False, gpu_ctx, ref), fitc_cap(Z, th),
+             "c5_sharded_p8")
+
+
 def test_fitc_shards_golden(gpu_ctx):
     """The reference-pinned golden case, 3 shards: same objectives as the dense reference."""
     g = load_golden("fitc_n2000_m200_rows")

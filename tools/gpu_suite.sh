@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-TAG=${TAG:-r3}
+TAG=${TAG:-r4}
 export GPS_PARITY_FLOORS=$PWD/gpurun_out/parity_floors_${TAG}.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/gpu_suite_${TAG}.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAILED|Error|error" gpurun_out/gpu_suite_${TAG}.log | head -30; tail -30 gpurun_out/gpu_suite_${TAG}.log; exit 1; }
 tail -2 gpurun_out/gpu_suite_${TAG}.log
