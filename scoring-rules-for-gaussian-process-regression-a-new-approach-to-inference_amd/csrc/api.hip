@@ -1909,12 +1909,16 @@ int fitc_syrk_rows(gps_ctx* ctx, const double* kscale, int ks, int64_t R0, int64
 // padded lower tiles.  With `packed` the sum goes lower-packed (m(m+1)/2, launch_sym_pack) into
 // dst instead: the payload of the ranks' all-reduce.
 int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* dst,
-              bool packed = false) {
+              bool packed = false, const double* A = nullptr, int64_t lda = 0) {
   const int64_t mp = ctx->m_pad;
   const int ks = fitc_syrk_ks(ctx);
   HIPCHK(ensure(ctx, ctx->slabB, (size_t)ks * mp * mp * 8));
+  if (!A) {  // the operand: Knm (default) or another n×m row panel (the whitened gradient's U, V)
+    A = ctx->Knm.d();
+    lda = mp;
+  }
   GemmParams p = gp0();
-  p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Knm.d(); p.ldb = mp;
+  p.A = A; p.lda = lda; p.B = A; p.ldb = lda;
   p.C = ctx->slabB.d(); p.ldc = mp; p.c_kslice_stride = mp * mp;
   p.M = (int)mp; p.N = (int)mp; p.K = (int)ctx->fn_pad; p.kscale = kscale;
   p.lower_out = 1; p.ksplit = ks;
@@ -2230,6 +2234,45 @@ int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_
   return 0;
 }
 
+// Whitened FITC gradient products (round 4; gps_fitc_grad, gps_fitc_blockloo).  The stored
+// factors ctx->Lm / ctx->Lb are the lower triangular inverses Lm⁻¹, Lb⁻¹ (m_pad², strict-upper
+// zero).  C (n_pad × m_pad, ldc) = Knm · Xᵀ for such an X: V = K Lm⁻ᵀ, U = K Lb⁻ᵀ.
+static int fitc_knm_xt(gps_ctx* ctx, int64_t ldc, const double* X, double* C) {
+  const int64_t mp = ctx->m_pad;
+  GemmParams p = gp0();
+  p.A = ctx->Knm.d(); p.lda = mp; p.B = X; p.ldb = mp; p.C = C; p.ldc = ldc;
+  p.M = (int)ctx->fn_pad; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+  return gemm(ctx, LAY_N, LAY_T, EPI_STORE, p);
+}
+// y (m_pad) = Xᵀ x for a stored lower X (m_pad²): the column reductions of X weighted by x, in
+// 256-row chunks through fslab (one chunk per 256 rows when fslab holds their partials)
+static int fitc_lt_vec(gps_ctx* ctx, const double* X, const double* x, double* y) {
+  const int64_t mp = ctx->m_pad;
+  const int64_t cap = (int64_t)(ctx->fslab.cap / 8);
+  int crows = 256;
+  while ((mp + crows - 1) / crows * mp * 2 > cap) crows *= 2;
+  HIPCHK(launch_colred(X, mp, (int)mp, (int)mp, 0, x, nullptr, y, nullptr, ctx->fslab.d(),
+                       ctx->stream, crows));
+  return 0;
+}
+// C (rows × m_pad) = A · X, X lower (k >= j)
+static int fitc_tri_right(gps_ctx* ctx, const double* A, int64_t lda, const double* X, double* C,
+                          int64_t ldc, int64_t rows) {
+  const int64_t mp = ctx->m_pad;
+  GemmParams p = gp0();
+  p.A = A; p.lda = lda; p.B = X; p.ldb = mp; p.C = C; p.ldc = ldc;
+  p.M = (int)rows; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_J;
+  return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
+}
+// C (m_pad²) = Xᵀ · B, X lower
+static int fitc_tri_left_t(gps_ctx* ctx, const double* X, const double* B, double* C) {
+  const int64_t mp = ctx->m_pad;
+  GemmParams p = gp0();
+  p.A = X; p.lda = mp; p.B = B; p.ldb = mp; p.C = C; p.ldc = mp;
+  p.M = (int)mp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_I;
+  return gemm(ctx, LAY_T, LAY_N, EPI_STORE, p);
+}
+
 // Objective value + analytic gradient of the FITC objectives w.r.t. θ and the inducing
 // inputs Z — the reference's fwd + `.backward()` at K20:236 (LOO-CRPS), K20:344 (NLML),
 // K20:452 (LOO-LogS); Z is a trained parameter there (K20:247).  Formulas: header of
@@ -2272,7 +2315,7 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
          *h = vbase + 4 * np, *hl2 = vbase + 5 * np, *md = vbase + 6 * np, *s1 = vbase + 7 * np,
          *s2 = vbase + 8 * np, *s3 = vbase + 9 * np, *zv = vbase + 10 * np;
   double* mb = ctx->fgm.d();
-  double *tku = mb, *tbt = mb + mp, *what = mb + 2 * mp;
+  double *tku = mb, *what = mb + 2 * mp;
   double* Bb = ctx->fgB.d();
   double *Binv = Bb, *Kminv = Bb + mp * mp, *Nm = Bb + 2 * mp * mp, *T1 = Bb + 3 * mp * mp,
          *KmD = Bb + 4 * mp * mp;
@@ -2295,34 +2338,32 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   const int64_t ldr = 3 * mp;
   HIPCHK(launch_fitc_grad_terms(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n, (int)np,
                                 objective, (double)ctx->fn_total, alpha, dinv, v, ulam, h, hl2, s));
-  // B⁻¹ = Lb⁻ᵀLb⁻¹, Km⁻¹ = Lm⁻ᵀLm⁻¹ (LAUUM, lower tiles) + mirror
-  const double* Ls[2] = {ctx->Lb.d(), ctx->Lm.d()};
-  double* Is[2] = {Binv, Kminv};
-  for (int w = 0; w < 2; ++w) {
-    GemmParams p = gp0();
-    p.A = Ls[w]; p.lda = mp; p.B = Ls[w]; p.ldb = mp; p.C = Is[w]; p.ldc = mp;
-    p.M = (int)mp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_I; p.lower_out = 1;
-    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
-    HIPCHK(launch_sym_mirror(Is[w], mp, (int)mp, s));
-  }
-  if (loo) {  // v = C⁻¹u = u/λ − (K B⁻¹ Kᵀ(u/λ))/λ
-    HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr,
-                         ctx->fslab.d(), s));
+  // Whitened (round 4, oracle.fast_fitc_grad): the operands are V = K Lm⁻ᵀ (R slot 2) and
+  // U = K Lb⁻ᵀ (slot 0), whose rows are bounded (‖V_i‖² = q_i ≤ sf², ‖U_i‖² = r_i); the explicit
+  // Km⁻¹ and B⁻¹ of round 3 (K·Km⁻¹, K·B⁻¹S2B⁻¹) amplified rounding by cond(B) ~1e7 on
+  // near-duplicate inducing points.
+  //   G_K  = Y Lb⁻¹ + diag(s3) V Lm⁻¹ − v cᵀ − α ŵᵀ,  Y = diag(s1) U + diag(s2) U P,
+  //   G_Km = −a(Km⁻¹ − B⁻¹) + Lb⁻ᵀ P Lb⁻¹ + Lm⁻ᵀ(Vᵀdiag(M_ii)V)Lm⁻¹ + ½(ŵcᵀ + cŵᵀ),
+  //   P = Uᵀ diag(h/λ²) U,  ŵ = Lm⁻ᵀ(Vᵀv),  v = u/λ − U(Uᵀ(u/λ))/λ.
+  double* U = R;
+  double* Yp = R + mp;
+  double* V = R + 2 * mp;
+  if ((rc = fitc_knm_xt(ctx, ldr, ctx->Lb.d(), U))) return rc;
+  if ((rc = fitc_knm_xt(ctx, ldr, ctx->Lm.d(), V))) return rc;
+  if (loo) {  // v = C⁻¹u = u/λ − U(Uᵀ(u/λ))/λ;  P = Uᵀ diag(h/λ²) U
+    HIPCHK(launch_colred(U, ldr, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr, ctx->fslab.d(), s));
     if ((rc = allreduce_sum(ctx, tku, (size_t)mp, s))) return rc;
-    HIPCHK(launch_gemv_full(Binv, mp, tku, tbt, (int)mp, (int)mp, s));
-    HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, tbt, zv, (int)np, (int)mp, s));
+    HIPCHK(launch_gemv_full(U, ldr, tku, zv, (int)np, (int)mp, s));
     HIPCHK(launch_fitc_grad_v(ulam, zv, ctx->lam.d(), (int)n, v, s));
-    // S2 = Kᵀ diag(h/λ²) K
-    if ((rc = fitc_syrk(ctx, hl2, nullptr, red, shard))) return rc;
+    if ((rc = fitc_syrk(ctx, hl2, nullptr, red, shard, U, ldr))) return rc;
   }
-  HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, v, nullptr, tw, nullptr,
-                       ctx->fslab.d(), s));  // Kᵀv
-  {  // LOO: [S2 | (Σ M_ii, not yet formed) | Kᵀv] in one call; NLML: Kᵀv.  Kᵀv is final here.
+  HIPCHK(launch_colred(V, ldr, (int)np, (int)mp, 0, v, nullptr, tw, nullptr, ctx->fslab.d(), s));
+  {  // LOO: [P | (Σ M_ii, not yet formed) | Vᵀv] in one call; NLML: Vᵀv.  Vᵀv is final here.
     double* r0 = loo ? red : tw;
     const size_t cnt = loo ? (size_t)(off_tw + mp) : (size_t)mp;
     if ((rc = allreduce_sum(ctx, r0, cnt, s))) return rc;
   }
-  HIPCHK(launch_gemv_full(Kminv, mp, tw, what, (int)mp, (int)mp, s));  // ŵ = Km⁻¹Kᵀv
+  if ((rc = fitc_lt_vec(ctx, ctx->Lm.d(), tw, what))) return rc;  // ŵ = Lm⁻ᵀ Vᵀv
   auto gemm_nn = [&](const double* A, int64_t lda, const double* B, double* C, int64_t ldc,
                      int M) -> int {
     GemmParams p = gp0();
@@ -2330,28 +2371,40 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
     p.M = M; p.N = (int)mp; p.K = (int)mp;
     return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
   };
-  if (loo) {  // N = B⁻¹ S2 B⁻¹
+  if (loo) {  // U P (slot 1) and N = Lb⁻ᵀ P Lb⁻¹ while P is in the reduction buffer
     if ((rc = sym_full())) return rc;
-    if ((rc = gemm_nn(Sfull, mp, Binv, T1, mp, (int)mp))) return rc;
-    if ((rc = gemm_nn(Binv, mp, T1, Nm, mp, (int)mp))) return rc;
+    if ((rc = gemm_nn(U, ldr, Sfull, Yp, ldr, (int)np))) return rc;
+    if ((rc = fitc_tri_right(ctx, Sfull, mp, ctx->Lb.d(), T1, mp, mp))) return rc;
+    if ((rc = fitc_tri_left_t(ctx, ctx->Lb.d(), T1, Nm))) return rc;
   }
-  // R = K·[B⁻¹ | N | Km⁻¹]
-  if ((rc = gemm_nn(ctx->Knm.d(), mp, Binv, R, ldr, (int)np))) return rc;
-  if (loo && (rc = gemm_nn(ctx->Knm.d(), mp, Nm, R + mp, ldr, (int)np))) return rc;
-  if ((rc = gemm_nn(ctx->Knm.d(), mp, Kminv, R + 2 * mp, ldr, (int)np))) return rc;
   {
     Prof pr(ctx, "fitc_grad_mdiag", 0, (loo ? 16.0 : 0.0) * np * mp);
-    HIPCHK(launch_fitc_grad_mdiag(loo ? R + mp : nullptr, ldr, ctx->Knm.d(), mp, (int)mp,
-                                  ctx->lam.d(), ctx->r.d(), dinv, alpha, v, loo ? h : nullptr, a,
-                                  (int)n, (int)np, md, s1, s2, s3, s));
+    HIPCHK(launch_fitc_grad_mdiag(loo ? Yp : nullptr, ldr, U, ldr, (int)mp, ctx->lam.d(), ctx->r.d(),
+                                  dinv, alpha, v, loo ? h : nullptr, a, (int)n, (int)np, md, s1, s2,
+                                  s3, s));
   }
-  // Kᵀ diag(M_ii) K and Σ M_ii (this shard) → all-reduce
-  if ((rc = fitc_syrk(ctx, md, nullptr, red, shard))) return rc;
+  // Y = diag(s1) U + diag(s2) U P (in slot 1), then Y Lb⁻¹ into slot 0 (U is done)
+  HIPCHK(launch_fitc_grad_y(U, loo ? Yp : nullptr, ldr, s1, s2, (int)np, (int)mp, Yp, s));
+  if ((rc = fitc_tri_right(ctx, Yp, ldr, ctx->Lb.d(), U, ldr, np))) return rc;
+  // Vᵀ diag(M_ii) V and Σ M_ii (this shard) → all-reduce;  then V Lm⁻¹ into slot 1
+  if ((rc = fitc_syrk(ctx, md, nullptr, red, shard, V, ldr))) return rc;
   HIPCHK(launch_dot(md, nullptr, (int)np, smd, s));
-  if ((rc = allreduce_sum(ctx, red, (size_t)(plen + 1), s))) return rc;  // [P | Σ M_ii], not Kᵀv
+  if ((rc = allreduce_sum(ctx, red, (size_t)(plen + 1), s))) return rc;  // [P2 | Σ M_ii], not Vᵀv
+  if ((rc = fitc_tri_right(ctx, V, ldr, ctx->Lm.d(), Yp, ldr, np))) return rc;
   if ((rc = sym_full())) return rc;
-  if ((rc = gemm_nn(Sfull, mp, Kminv, T1, mp, (int)mp))) return rc;
-  if ((rc = gemm_nn(Kminv, mp, T1, KmD, mp, (int)mp))) return rc;
+  if ((rc = fitc_tri_right(ctx, Sfull, mp, ctx->Lm.d(), T1, mp, mp))) return rc;
+  if ((rc = fitc_tri_left_t(ctx, ctx->Lm.d(), T1, KmD))) return rc;
+  if (a != 0.0) {  // NLML: B⁻¹ = Lb⁻ᵀLb⁻¹, Km⁻¹ = Lm⁻ᵀLm⁻¹ (LAUUM, lower tiles) + mirror
+    const double* Ls[2] = {ctx->Lb.d(), ctx->Lm.d()};
+    double* Is[2] = {Binv, Kminv};
+    for (int w = 0; w < 2; ++w) {
+      GemmParams p = gp0();
+      p.A = Ls[w]; p.lda = mp; p.B = Ls[w]; p.ldb = mp; p.C = Is[w]; p.ldc = mp;
+      p.M = (int)mp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_I; p.lower_out = 1;
+      if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+      HIPCHK(launch_sym_mirror(Is[w], mp, (int)mp, s));
+    }
+  }
   // contraction with ∂Knm/∂θ, ∂Knm/∂Z
   FitcContractParams cp;
   memset(&cp, 0, sizeof(cp));
@@ -2362,12 +2415,11 @@ int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
   {
     FitcContractParams p = cp;
     p.xr = ctx->fX.d(); p.xc = ctx->Z.d(); p.nr = (int)n; p.nc = (int)m; p.nc_pad = (int)mp;
-    p.R[p.nt] = R; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s1;
-    if (loo) { p.R[p.nt] = R + mp; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s2; }
-    p.R[p.nt] = R + 2 * mp; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s3;
+    p.R[p.nt] = U; p.ldr[p.nt] = ldr; p.coef[p.nt++] = 1.0;                      // Y Lb⁻¹
+    p.R[p.nt] = Yp; p.ldr[p.nt] = ldr; p.coef[p.nt] = 1.0; p.rs[p.nt++] = s3;    // V Lm⁻¹
     p.pc[0] = -1.0; p.pv[0] = v; p.qv[0] = ctx->c.d();
     p.pc[1] = -1.0; p.pv[1] = alpha; p.qv[1] = what;
-    Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * (loo ? 3 : 2) * np * mp);
+    Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * 2 * np * mp);
     HIPCHK(launch_fitc_grad_contract(p, out1, out1 + passes * 17, s));
   }
   if ((rc = allreduce_sum(ctx, out1, (size_t)outlen, s))) return rc;
@@ -2656,16 +2708,17 @@ static int local_folds(gps_ctx* ctx, int nfold, std::vector<int64_t>& bnd, std::
 }
 
 // FITC block-LOO objective (K20:523-587 DSS, K20:655-720 KC): P_f = ((Q+Λ)⁻¹)_ff =
-// Λ_f⁻¹ − U_fU_fᵀ with U = Λ⁻¹K Lb⁻ᵀ (one n×m TRMM), α = (y − Kc)/λ.  With grad / grad_z the
+// Λ_f⁻¹ − Ũ_fŨ_fᵀ with Ũ = Λ⁻¹K Lb⁻ᵀ (one n×m TRMM), α = (y − Kc)/λ.  With grad / grad_z the
 // `.backward()` at K20:587 / 720 w.r.t. θ and the inducing inputs (moved at K20:593 / 726):
-// M = −C⁻¹GblkC⁻¹ − ½(vαᵀ + αvᵀ), v = C⁻¹g (C = Q + Λ); Woodbury with E = Λ⁻¹KB⁻¹ = C⁻¹KKm⁻¹:
-//   F = Gblk E (one b×b×m GEMM per fold), S = EᵀF, T = KᵀΛ⁻¹F (n·m² each),
-//   G_K  = −2Λ⁻¹F + 2Λ⁻¹K(B⁻¹T) − 2diag(M_ii)KKm⁻¹ − vcᵀ − αŵᵀ,  ŵ = Km⁻¹Kᵀv,
-//   G_Km = S + Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹ + ½(ŵcᵀ + cŵᵀ),
-//   M_ii = −(G_ii − 2F_i·K_i + (KS)_i·K_i)/λ_i² − v_iα_i   (blk_mdiag, kernels_block.hip),
-// contracted with ∂K/∂θ, ∂K/∂Z like gps_fitc_grad.  Row-sharded like gps_fitc_grad when every
-// fold lies in one rank's rows (local_folds): the folds are local, the fold values and the
-// n-sums Kᵀ(g/λ), [S | T], Kᵀv, [Kᵀdiag(M_ii)K | ΣM_ii] and the contraction are all-reduced.
+// M = −C⁻¹GblkC⁻¹ − ½(vαᵀ + αvᵀ), v = C⁻¹g (C = Q + Λ), whitened (round 4, no explicit B⁻¹ or
+// Km⁻¹; oracle.fast_fitc_blockloo): F̃ = Gblk Ũ (one b×b×m GEMM per fold), S̃ = ŨᵀF̃ (n·m²),
+//   G_K  = (−2Λ⁻¹F̃ + 2ŨS̃) Lb⁻¹ − 2diag(M_ii) V Lm⁻¹ − vcᵀ − αŵᵀ,  V = K Lm⁻ᵀ, ŵ = Lm⁻ᵀVᵀv,
+//   G_Km = Lb⁻ᵀS̃Lb⁻¹ + Lm⁻ᵀ(Vᵀdiag(M_ii)V)Lm⁻¹ + ½(ŵcᵀ + cŵᵀ),
+//   M_ii = −G_ii/λ_i² + 2F̃_i·Ũ_i/λ_i − (ŨS̃)_i·Ũ_i − v_iα_i   (blk_mdiag, kernels_block.hip),
+// contracted with ∂K/∂θ, ∂K/∂Z like gps_fitc_grad (9·n·m² GEMM flops; round 3's explicit-inverse
+// form took 14).  Row-sharded like gps_fitc_grad when every fold lies in one rank's rows
+// (local_folds): the folds are local, the fold values and the n-sums Ũᵀg, S̃, Vᵀv,
+// [Vᵀdiag(M_ii)V | ΣM_ii] and the contraction are all-reduced.
 int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, int objective,
                       double* value, double* grad, double* grad_z, double* fold_values) {
   if (int rc = bind(ctx)) return rc;
@@ -2686,51 +2739,28 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   if ((rc = local_folds(ctx, nfold, bnd, fid))) return rc;
   hipStream_t s = ctx->stream;
   const bool want = grad != nullptr || grad_z != nullptr;
-  const int64_t ldr = want ? 3 * mp : mp;  // [U | E | K Km⁻¹]; U's slot later holds KS, KB⁻¹T
+  const int64_t ldr = want ? 3 * mp : mp;  // [Ũ → Y Lb⁻¹ | ŨS̃ → Y → V Lm⁻¹ | V]
   const int64_t bp = bounds_pad(bnd);
   HIPCHK(ensure(ctx, ctx->fR, (size_t)np * ldr * 8));
   HIPCHK(ensure(ctx, ctx->fgv, (size_t)13 * np * 8));
   double* U = ctx->fR.d();
-  double* E = U + mp;
-  double* RC = U + 2 * mp;
   double* vb = ctx->fgv.d();
   double *alpha = vb, *dinv = vb + np, *v = vb + 2 * np, *ulam = vb + 3 * np, *hh = vb + 4 * np,
          *hl2 = vb + 5 * np, *gg = vb + 6 * np, *gd = vb + 7 * np, *md = vb + 8 * np,
-         *sa = vb + 9 * np, *sb = vb + 10 * np, *scl = vb + 11 * np, *zv = vb + 12 * np;
+         *scl = vb + 11 * np, *zv = vb + 12 * np;
   HIPCHK(launch_fitc_grad_terms(ctx->fy.d(), ctx->lam.d(), ctx->r.d(), ctx->g.d(), (int)n, (int)np,
                                 GPS_OBJ_NLML, (double)n, alpha, dinv, v, ulam, hh, hl2, s));
-  {  // U = Λ⁻¹ K Lb⁻ᵀ
-    GemmParams p = gp0();
-    p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp; p.C = U; p.ldc = ldr;
-    p.M = (int)np; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
-    if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
-    HIPCHK(launch_row_scale(U, ldr, (int)np, (int)mp, ctx->ilam.d(), s));
-  }
-  auto gemm_nn = [&](const double* A, int64_t lda, const double* B, double* C, int64_t ldc,
-                     int64_t rows) -> int {
-    GemmParams p = gp0();
-    p.A = A; p.lda = lda; p.B = B; p.ldb = mp; p.C = C; p.ldc = ldc;
-    p.M = (int)rows; p.N = (int)mp; p.K = (int)mp;
-    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
-  };
-  double *Binv = nullptr, *Kminv = nullptr, *Sm = nullptr, *Tm = nullptr, *BT = nullptr,
-         *KmD = nullptr, *F = nullptr;
+  // Ũ = Λ⁻¹ K Lb⁻ᵀ
+  if ((rc = fitc_knm_xt(ctx, ldr, ctx->Lb.d(), U))) return rc;
+  HIPCHK(launch_row_scale(U, ldr, (int)np, (int)mp, ctx->ilam.d(), s));
+  // gradient buffers (whitened, round 4; oracle.fast_fitc_blockloo): R slots [Ũ | ŨS̃ → Y | V]
+  double *Sm = nullptr, *T1 = nullptr, *Sfin = nullptr, *KmD = nullptr, *F = nullptr;
+  double* US = U + mp;
+  double* V = U + 2 * mp;
   if (want) {
-    HIPCHK(ensure(ctx, ctx->fgB, (size_t)(shard ? 7 : 6) * mp * mp * 8));
+    HIPCHK(ensure(ctx, ctx->fgB, (size_t)(shard ? 5 : 4) * mp * mp * 8));
     double* Bb = ctx->fgB.d();
-    Binv = Bb; Kminv = Bb + mp * mp; Sm = Bb + 2 * mp * mp; Tm = Bb + 3 * mp * mp;
-    BT = Bb + 4 * mp * mp; KmD = Bb + 5 * mp * mp;
-    const double* Ls[2] = {ctx->Lb.d(), ctx->Lm.d()};
-    double* Is[2] = {Binv, Kminv};
-    for (int q = 0; q < 2; ++q) {  // B⁻¹, Km⁻¹ (LAUUM, lower tiles) + mirror
-      GemmParams p = gp0();
-      p.A = Ls[q]; p.lda = mp; p.B = Ls[q]; p.ldb = mp; p.C = Is[q]; p.ldc = mp;
-      p.M = (int)mp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_GE_I; p.lower_out = 1;
-      if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
-      HIPCHK(launch_sym_mirror(Is[q], mp, (int)mp, s));
-    }
-    if ((rc = gemm_nn(ctx->Knm.d(), mp, Binv, E, ldr, np))) return rc;  // E = Λ⁻¹ K B⁻¹
-    HIPCHK(launch_row_scale(E, ldr, (int)np, (int)mp, ctx->ilam.d(), s));
+    Sm = Bb; T1 = Bb + mp * mp; Sfin = Bb + 2 * mp * mp; KmD = Bb + 3 * mp * mp;
     HIPCHK(ensure(ctx, ctx->bF, (size_t)np * mp * 8));
     HIPCHK(ensure(ctx, ctx->bEf, (size_t)bp * mp * 8));
     HIPCHK(ensure(ctx, ctx->bFf, (size_t)bp * mp * 8));
@@ -2752,12 +2782,12 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     return 0;
   };
   auto gdst = [&](int64_t, int64_t) { return std::make_pair(ctx->bG.d(), bp); };
-  auto gdone = [&](int, int64_t a, int64_t b) -> int {  // F rows of the fold = G_f E_f; diag G_f
-    double* Ef = ctx->bEf.d();
+  auto gdone = [&](int, int64_t a, int64_t b) -> int {  // F̃ rows of the fold = G_f Ũ_f; diag G_f
+    double* Uf = ctx->bEf.d();
     double* Ff = ctx->bFf.d();
-    HIPCHK(launch_pad_copy(E + a * ldr, ldr, Ef, mp, (int)b, (int)mp, (int)bp, (int)mp, 0, s));
+    HIPCHK(launch_pad_copy(U + a * ldr, ldr, Uf, mp, (int)b, (int)mp, (int)bp, (int)mp, 0, s));
     GemmParams p = gp0();
-    p.A = ctx->bG.d(); p.lda = bp; p.B = Ef; p.ldb = mp; p.C = Ff; p.ldc = mp;
+    p.A = ctx->bG.d(); p.lda = bp; p.B = Uf; p.ldb = mp; p.C = Ff; p.ldc = mp;
     p.M = (int)bp; p.N = (int)mp; p.K = (int)bp;
     if (int rc2 = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p)) return rc2;
     HIPCHK(launch_pad_copy(Ff, mp, F + a * mp, mp, (int)b, (int)mp, (int)b, (int)mp, 0, s));
@@ -2781,39 +2811,37 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   if (fold_values)
     for (int f = 0; f < nfold; ++f) fold_values[f] = fv[f];
   if (!want) return 0;
-  // v = C⁻¹g = g/λ − Λ⁻¹K B⁻¹Kᵀ(g/λ)
+  // v = C⁻¹g = g/λ − Ũ(Ũᵀg)
   HIPCHK(ensure(ctx, ctx->fgm, (size_t)6 * mp * 8));
   double* mb = ctx->fgm.d();
-  double *tku = mb, *tbt = mb + mp, *what = mb + 2 * mp;
+  double *tku = mb, *what = mb + 2 * mp;
   HIPCHK(launch_vec_mul(gg, ctx->ilam.d(), (int)np, ulam, s));
-  HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, ulam, nullptr, tku, nullptr,
-                       ctx->fslab.d(), s));
+  HIPCHK(launch_colred(U, ldr, (int)np, (int)mp, 0, gg, nullptr, tku, nullptr, ctx->fslab.d(), s));
   if ((rc = allreduce_sum(ctx, tku, (size_t)mp, s))) return rc;
-  HIPCHK(launch_gemv_full(Binv, mp, tku, tbt, (int)mp, (int)mp, s));
-  HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, tbt, zv, (int)np, (int)mp, s));
-  HIPCHK(launch_fitc_grad_v(ulam, zv, ctx->lam.d(), (int)n, v, s));
-  {  // T = KᵀΛ⁻¹F, S = EᵀF (m×m, n·m² each; [S | T] contiguous: one all-reduce)
-    GemmParams p = gp0();
-    p.A = ctx->Knm.d(); p.lda = mp; p.B = F; p.ldb = mp; p.C = Tm; p.ldc = mp;
-    p.kscale = ctx->ilam.d(); p.M = (int)mp; p.N = (int)mp; p.K = (int)np;
-    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+  HIPCHK(launch_gemv_full(U, ldr, tku, zv, (int)np, (int)mp, s));
+  HIPCHK(launch_fitc_grad_v(ulam, zv, nullptr, (int)n, v, s));
+  {  // S̃ = ŨᵀF̃ (n·m²), all-reduced
     GemmParams q = gp0();
-    q.A = E; q.lda = ldr; q.B = F; q.ldb = mp; q.C = Sm; q.ldc = mp;
+    q.A = U; q.lda = ldr; q.B = F; q.ldb = mp; q.C = Sm; q.ldc = mp;
     q.M = (int)mp; q.N = (int)mp; q.K = (int)np;
     if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, q))) return rc;
   }
-  if ((rc = allreduce_sum(ctx, Sm, (size_t)2 * mp * mp, s))) return rc;
-  if ((rc = gemm_nn(Binv, mp, Tm, BT, mp, mp))) return rc;          // B⁻¹T
-  if ((rc = gemm_nn(ctx->Knm.d(), mp, Sm, U, ldr, np))) return rc;  // K S (into U's slot)
-  {
-    Prof pr(ctx, "blk_mdiag", 0, 24.0 * np * mp);
-    HIPCHK(launch_blk_mdiag(F, mp, U, ldr, ctx->Knm.d(), mp, (int)mp, gd, ctx->lam.d(), v, alpha,
-                            (int)n, (int)np, md, sa, sb, scl, s));
+  if ((rc = allreduce_sum(ctx, Sm, (size_t)mp * mp, s))) return rc;
+  {  // ŨS̃ into slot 1
+    GemmParams p = gp0();
+    p.A = U; p.lda = ldr; p.B = Sm; p.ldb = mp; p.C = US; p.ldc = ldr;
+    p.M = (int)np; p.N = (int)mp; p.K = (int)mp;
+    if ((rc = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p))) return rc;
   }
-  if ((rc = gemm_nn(ctx->Knm.d(), mp, BT, U, ldr, np))) return rc;      // K B⁻¹T
-  if ((rc = gemm_nn(ctx->Knm.d(), mp, Kminv, RC, ldr, np))) return rc;  // K Km⁻¹
-  // ŵ = Km⁻¹Kᵀv;  Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹;  Σ M_ii
-  // [P | Σ M_ii | (pad) | Kᵀv]: P = Kᵀdiag(M_ii)K lower-packed (m(m+1)/2) when sharded, else
+  {  // M_ii, the V Lm⁻¹ row scale, and Y = −2Λ⁻¹F̃ + 2ŨS̃ over slot 1 — one pass over F̃, ŨS̃, Ũ
+    Prof pr(ctx, "blk_mdiag", 0, 32.0 * np * mp);
+    HIPCHK(launch_blk_mdiag(F, mp, US, ldr, U, ldr, (int)mp, gd, ctx->lam.d(), v, alpha, (int)n,
+                            (int)np, md, scl, US, ldr, s));
+  }
+  if ((rc = fitc_tri_right(ctx, US, ldr, ctx->Lb.d(), U, ldr, np))) return rc;  // Y Lb⁻¹ → slot 0
+  if ((rc = fitc_knm_xt(ctx, ldr, ctx->Lm.d(), V))) return rc;                  // V = K Lm⁻ᵀ
+  // ŵ = Lm⁻ᵀVᵀv;  Lm⁻ᵀ(Vᵀdiag(M_ii)V)Lm⁻¹;  Σ M_ii
+  // [P | Σ M_ii | (pad) | Vᵀv]: P = Vᵀdiag(M_ii)V lower-packed (m(m+1)/2) when sharded, else
   // the padded lower tiles (gps_fitc_grad's layout)
   HIPCHK(ensure(ctx, ctx->fgred, (size_t)(mp * mp + 2 * mp + 64) * 8));
   const int64_t plen = shard ? m * (m + 1) / 2 : mp * mp;
@@ -2821,22 +2849,24 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   double* red = ctx->fgred.d();
   double* smd = red + plen;
   double* tw = red + off_tw;
-  HIPCHK(launch_colred(ctx->Knm.d(), mp, (int)np, (int)mp, 0, v, nullptr, tw, nullptr,
-                       ctx->fslab.d(), s));
+  HIPCHK(launch_colred(V, ldr, (int)np, (int)mp, 0, v, nullptr, tw, nullptr, ctx->fslab.d(), s));
   if ((rc = allreduce_sum(ctx, tw, (size_t)mp, s))) return rc;
-  HIPCHK(launch_gemv_full(Kminv, mp, tw, what, (int)mp, (int)mp, s));
-  if ((rc = fitc_syrk(ctx, md, nullptr, red, shard))) return rc;
+  if ((rc = fitc_lt_vec(ctx, ctx->Lm.d(), tw, what))) return rc;  // ŵ = Lm⁻ᵀ Vᵀv
+  if ((rc = fitc_syrk(ctx, md, nullptr, red, shard, V, ldr))) return rc;
   HIPCHK(launch_dot(md, nullptr, (int)np, smd, s));
   if ((rc = allreduce_sum(ctx, red, (size_t)(plen + 1), s))) return rc;
   double* Pfull = red;
   if (shard) {
-    Pfull = ctx->fgB.d() + 6 * mp * mp;
+    Pfull = ctx->fgB.d() + 4 * mp * mp;
     HIPCHK(launch_sym_unpack(red, (int)m, (int)mp, nullptr, 1, Pfull, s));
   } else {
     HIPCHK(launch_sym_mirror(red, mp, (int)mp, s));
   }
-  if ((rc = gemm_nn(Pfull, mp, Kminv, Tm, mp, mp))) return rc;
-  if ((rc = gemm_nn(Kminv, mp, Tm, KmD, mp, mp))) return rc;
+  if ((rc = fitc_tri_right(ctx, V, ldr, ctx->Lm.d(), US, ldr, np))) return rc;  // V Lm⁻¹ → slot 1
+  if ((rc = fitc_tri_right(ctx, Pfull, mp, ctx->Lm.d(), T1, mp, mp))) return rc;
+  if ((rc = fitc_tri_left_t(ctx, ctx->Lm.d(), T1, KmD))) return rc;
+  if ((rc = fitc_tri_right(ctx, Sm, mp, ctx->Lb.d(), T1, mp, mp))) return rc;   // Lb⁻ᵀS̃Lb⁻¹
+  if ((rc = fitc_tri_left_t(ctx, ctx->Lb.d(), T1, Sfin))) return rc;
   // contractions with ∂Knm/∂θ, ∂Knm/∂Z and ∂Kmm/∂θ, ∂Kmm/∂Z
   const int passes = fitc_contract_passes(d);
   const int64_t outlen = (int64_t)passes * 17 + m * d;
@@ -2854,20 +2884,19 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   {
     FitcContractParams p = cp;
     p.xr = ctx->fX.d(); p.xc = ctx->Z.d(); p.nr = (int)n; p.nc = (int)m; p.nc_pad = (int)mp;
-    p.R[0] = F; p.ldr[0] = mp; p.coef[0] = 1.0; p.rs[0] = sa;
-    p.R[1] = U; p.ldr[1] = ldr; p.coef[1] = 1.0; p.rs[1] = sb;
-    p.R[2] = RC; p.ldr[2] = ldr; p.coef[2] = 1.0; p.rs[2] = scl;
-    p.nt = 3;
+    p.R[0] = U; p.ldr[0] = ldr; p.coef[0] = 1.0;                  // Y Lb⁻¹
+    p.R[1] = US; p.ldr[1] = ldr; p.coef[1] = 1.0; p.rs[1] = scl;  // −2diag(M_ii) V Lm⁻¹
+    p.nt = 2;
     p.pc[0] = -1.0; p.pv[0] = v; p.qv[0] = ctx->c.d();
     p.pc[1] = -1.0; p.pv[1] = alpha; p.qv[1] = what;
-    Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * 3 * np * mp);
+    Prof pr(ctx, "fitc_grad_contract", 0, 8.0 * 2 * np * mp);
     HIPCHK(launch_fitc_grad_contract(p, out1, out1 + passes * 17, s));
   }
   if ((rc = allreduce_sum(ctx, out1, (size_t)outlen, s))) return rc;
   {  // the m×m contraction: every operand is global by now (replicated on every rank)
     FitcContractParams p = cp;
     p.xr = ctx->Z.d(); p.xc = ctx->Z.d(); p.nr = (int)m; p.nc = (int)m; p.nc_pad = (int)mp;
-    p.R[0] = Sm; p.ldr[0] = mp; p.coef[0] = 1.0;
+    p.R[0] = Sfin; p.ldr[0] = mp; p.coef[0] = 1.0;
     p.R[1] = KmD; p.ldr[1] = mp; p.coef[1] = 1.0;
     p.nt = 2;
     p.pc[0] = 0.5; p.pv[0] = what; p.qv[0] = ctx->c.d();

@@ -298,11 +298,12 @@ hipError_t launch_add_diag(double* P, int64_t ld, const double* vals, int nreal,
 hipError_t launch_row_scale(double* M, int64_t ld, int rows, int cols, const double* scale,
                             hipStream_t s);
 hipError_t launch_vec_mul(const double* a, const double* b, int n, double* out, hipStream_t s);
-// FITC block-LOO gradient: M_ii and the row scales of G_K (see kernels_block.hip)
-hipError_t launch_blk_mdiag(const double* F, int64_t ldf, const double* KS, int64_t ldks,
-                            const double* K, int64_t ldk, int m_pad, const double* gd,
+// FITC block-LOO gradient (whitened): M_ii, the V Lm⁻¹ row scale and Y = −2Λ⁻¹F̃ + 2ŨS̃
+// (see kernels_block.hip; Y may alias US)
+hipError_t launch_blk_mdiag(const double* F, int64_t ldf, const double* US, int64_t ldus,
+                            const double* U, int64_t ldu, int m_pad, const double* gd,
                             const double* lam, const double* v, const double* alpha, int n,
-                            int n_pad, double* md, double* sa, double* sb, double* sc,
+                            int n_pad, double* md, double* sc, double* Y, int64_t ldy,
                             hipStream_t s);
 // energy score: Newton–Schulz steps, distances, reduction
 hipError_t launch_ns_init(const double* C, int64_t ldc, int b, int bp, double scale, double pad,
@@ -331,6 +332,8 @@ hipError_t launch_fitc_grad_mdiag(const double* KN, int64_t ldkn, const double* 
                                   const double* alpha, const double* v, const double* h, double a,
                                   int n, int n_pad, double* mdiag, double* s1, double* s2,
                                   double* s3, hipStream_t s);
+hipError_t launch_fitc_grad_y(const double* U, const double* UP, int64_t ld, const double* s1,
+                              const double* s2, int rows, int cols, double* Y, hipStream_t s);
 int fitc_contract_passes(int d);
 int64_t fitc_contract_slab_doubles(int nr, int nc_pad, int d);
 // out[pass*17 + q]: q = 0 Σ GK, 1+k Σ GK Δ²_(16·pass+k);  zout[j*d + k] = Σ_i GK Δ_k (real j)

@@ -127,57 +127,59 @@ hipError_t launch_vec_mul(const double* a, const double* b, int n, double* out, 
 }
 
 // ------------------------------------------- FITC block-LOO gradient (K20:587, K20:720)
-// With M = −C⁻¹GblkC⁻¹ − ½(vαᵀ + αvᵀ), E = Λ⁻¹KB⁻¹, F = Gblk E, S = EᵀF (api.hip):
-//   M_ii = −(G_ii − 2 F_i·K_i + (K S)_i·K_i)/λ_i² − v_iα_i
-// and the row scales of G_K = −2Λ⁻¹F + 2Λ⁻¹K(B⁻¹T) − 2diag(M_ii)KKm⁻¹ − (vcᵀ + αŵᵀ):
-// sa = −2/λ, sb = 2/λ, sc = −2M_ii.  One wave per row (HBM-bound: reads F, KS, K once);
-// pad rows get zeros.
+// Whitened (round 4, api.hip gps_fitc_blockloo): with Ũ = Λ⁻¹K Lb⁻ᵀ, F̃ = Gblk Ũ, S̃ = ŨᵀF̃,
+//   M_ii = −G_ii/λ_i² + 2 F̃_i·Ũ_i/λ_i − (ŨS̃)_i·Ũ_i − v_iα_i,
+// the row scale of G_K's V Lm⁻¹ term sc = −2M_ii, and the left factor of its Lb⁻¹ term
+// Y = −2Λ⁻¹F̃ + 2ŨS̃ (written over Y, which may alias US: each element is read, then written, by
+// the same lane).  One wave per row (HBM-bound: one pass over F̃, ŨS̃, Ũ); pad rows get zeros.
 __global__ __launch_bounds__(256) void blk_mdiag_kernel(
-    const double* __restrict__ F, int64_t ldf, const double* __restrict__ KS, int64_t ldks,
-    const double* __restrict__ K, int64_t ldk, int m_pad, const double* __restrict__ gd,
+    const double* __restrict__ F, int64_t ldf, const double* US, int64_t ldus,
+    const double* __restrict__ U, int64_t ldu, int m_pad, const double* __restrict__ gd,
     const double* __restrict__ lam, const double* __restrict__ v,
     const double* __restrict__ alpha, int n, int n_pad, double* __restrict__ md,
-    double* __restrict__ sa, double* __restrict__ sb, double* __restrict__ sc) {
+    double* __restrict__ sc, double* Y, int64_t ldy) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n_pad) return;
+  double* y = Y + (int64_t)i * ldy;
   if (i >= n) {
-    if (lane == 0) md[i] = sa[i] = sb[i] = sc[i] = 0.0;
+    if (lane == 0) md[i] = sc[i] = 0.0;
+    for (int j = 2 * lane; j < m_pad; j += 128) *reinterpret_cast<double2*>(y + j) = double2{0.0, 0.0};
     return;
   }
   const double* f = F + (int64_t)i * ldf;
-  const double* ks = KS + (int64_t)i * ldks;
-  const double* k = K + (int64_t)i * ldk;
+  const double* us = US + (int64_t)i * ldus;
+  const double* u = U + (int64_t)i * ldu;
+  const double il = 1.0 / lam[i];
   double p = 0.0, q = 0.0;
   for (int j = 2 * lane; j < m_pad; j += 128) {
-    const double2 kv = *reinterpret_cast<const double2*>(k + j);
+    const double2 uv = *reinterpret_cast<const double2*>(u + j);
     const double2 fv = *reinterpret_cast<const double2*>(f + j);
-    const double2 sv = *reinterpret_cast<const double2*>(ks + j);
-    p = fma(fv.x, kv.x, p);
-    p = fma(fv.y, kv.y, p);
-    q = fma(sv.x, kv.x, q);
-    q = fma(sv.y, kv.y, q);
+    const double2 sv = *reinterpret_cast<const double2*>(us + j);
+    p = fma(fv.x, uv.x, p);
+    p = fma(fv.y, uv.y, p);
+    q = fma(sv.x, uv.x, q);
+    q = fma(sv.y, uv.y, q);
+    *reinterpret_cast<double2*>(y + j) =
+        double2{fma(-2.0 * il, fv.x, 2.0 * sv.x), fma(-2.0 * il, fv.y, 2.0 * sv.y)};
   }
   p = wave_sum(p);
   q = wave_sum(q);
   if (lane == 0) {
-    const double il = 1.0 / lam[i];
-    const double mi = -(gd[i] - 2.0 * p + q) * il * il - v[i] * alpha[i];
+    const double mi = -gd[i] * il * il + 2.0 * p * il - q - v[i] * alpha[i];
     md[i] = mi;
-    sa[i] = -2.0 * il;
-    sb[i] = 2.0 * il;
     sc[i] = -2.0 * mi;
   }
 }
 
-hipError_t launch_blk_mdiag(const double* F, int64_t ldf, const double* KS, int64_t ldks,
-                            const double* K, int64_t ldk, int m_pad, const double* gd,
+hipError_t launch_blk_mdiag(const double* F, int64_t ldf, const double* US, int64_t ldus,
+                            const double* U, int64_t ldu, int m_pad, const double* gd,
                             const double* lam, const double* v, const double* alpha, int n,
-                            int n_pad, double* md, double* sa, double* sb, double* sc,
+                            int n_pad, double* md, double* sc, double* Y, int64_t ldy,
                             hipStream_t s) {
-  if ((ldf & 1) || (ldks & 1) || (ldk & 1) || (m_pad & 1)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(blk_mdiag_kernel, dim3((n_pad + 3) / 4), dim3(256), 0, s, F, ldf, KS, ldks, K,
-                     ldk, m_pad, gd, lam, v, alpha, n, n_pad, md, sa, sb, sc);
+  if ((ldf & 1) || (ldus & 1) || (ldu & 1) || (ldy & 1) || (m_pad & 1)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(blk_mdiag_kernel, dim3((n_pad + 3) / 4), dim3(256), 0, s, F, ldf, US, ldus, U,
+                     ldu, m_pad, gd, lam, v, alpha, n, n_pad, md, sc, Y, ldy);
   return hipGetLastError();
 }
 

@@ -6,8 +6,10 @@
 //   C = Q + Λ, Q = K Km⁻¹ Kᵀ (K = Knm, Km = K(Z,Z) + 1e-3·I), Λ = diag(K_ff − Q) + σ²I
 //   ∂obj = tr(M ∂C),  M = a·C⁻¹ − ½(vαᵀ + αvᵀ) − C⁻¹ diag(h) C⁻¹
 //   tr(M ∂C) = Σ G_K ∘ ∂K + Σ G_Km ∘ ∂Km + Σ_i M_ii (∂K_ii + ∂σ²)
-//   G_K  = s1 ∘ (K B⁻¹) + s2 ∘ (K N) + s3 ∘ (K Km⁻¹) − v cᵀ − α ŵᵀ      (row scales s1..s3)
-//   G_Km = a(B⁻¹ − Km⁻¹) + N + Km⁻¹(Kᵀdiag(M_ii)K)Km⁻¹ + ½(ŵcᵀ + cŵᵀ)
+//   G_K  = (s1 ∘ U + s2 ∘ U P) Lb⁻¹ + s3 ∘ (V Lm⁻¹) − v cᵀ − α ŵᵀ      (row scales s1..s3)
+//   G_Km = a(B⁻¹ − Km⁻¹) + Lb⁻ᵀ P Lb⁻¹ + Lm⁻ᵀ(Vᵀdiag(M_ii)V)Lm⁻¹ + ½(ŵcᵀ + cŵᵀ)
+// whitened (round 4): U = K Lb⁻ᵀ, V = K Lm⁻ᵀ, P = Uᵀdiag(h/λ²)U — no explicit Km⁻¹ / B⁻¹ in the
+// n×m products (K B⁻¹ = U Lb⁻¹, K Km⁻¹ = V Lm⁻¹, K N = U P Lb⁻¹)
 // The m×m and n×m products run in the MFMA GEMM (api.hip); this file holds the per-row
 // terms and the contraction of G with ∂K/∂θ and ∂K/∂Z, which recomputes K_ij and the
 // scaled differences from the features instead of storing d+2 derivative matrices.
@@ -71,13 +73,13 @@ hipError_t launch_fitc_grad_terms(const double* y, const double* lam, const doub
   return hipGetLastError();
 }
 
-// v = ulam − z/λ  (v = C⁻¹u by Woodbury, z = K B⁻¹ Kᵀ(u/λ))
+// v = ulam − z/λ  (v = C⁻¹u by Woodbury, z = U Uᵀ(u/λ)); lam NULL: v = ulam − z
 __global__ __launch_bounds__(256) void fitc_grad_v_kernel(const double* __restrict__ ulam,
                                                           const double* __restrict__ z,
                                                           const double* __restrict__ lam, int n,
                                                           double* __restrict__ v) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) v[i] = ulam[i] - z[i] / lam[i];
+  if (i < n) v[i] = ulam[i] - (lam ? z[i] / lam[i] : z[i]);
 }
 
 hipError_t launch_fitc_grad_v(const double* ulam, const double* z, const double* lam, int n,
@@ -87,7 +89,7 @@ hipError_t launch_fitc_grad_v(const double* ulam, const double* z, const double*
   return hipGetLastError();
 }
 
-// One wave per row: q_i = Σ_j (K N)_ij K_ij (skipped when KN is null: h = 0), then
+// One wave per row: q_i = Σ_j (U P)_ij U_ij = k_i N k_iᵀ (skipped when KN is null: h = 0), then
 //   M_ii = a·d_i − v_iα_i − (h_i/λ_i² − 2h_i r_i/λ_i³ + q_i/λ_i²)
 //   s1 = 2(a/λ − h/λ²), s2 = 2/λ, s3 = −2 M_ii  (row scales of G_K); pad rows: all 0.
 __global__ __launch_bounds__(256) void fitc_grad_mdiag_kernel(
@@ -134,6 +136,38 @@ hipError_t launch_fitc_grad_mdiag(const double* KN, int64_t ldkn, const double* 
                                   double* s3, hipStream_t s) {
   hipLaunchKernelGGL(fitc_grad_mdiag_kernel, dim3((n_pad + 3) / 4), dim3(256), 0, s, KN, ldkn, K,
                      ldk, m_pad, lam, r, dinv, alpha, v, h, a, n, n_pad, mdiag, s1, s2, s3);
+  return hipGetLastError();
+}
+
+// Y = diag(s1)·U + diag(s2)·UP over rows × cols (UP null: the s2 term is absent); Y may alias UP
+// (the whitened G_K's left factor, api.hip gps_fitc_grad)
+__global__ __launch_bounds__(256) void fitc_grad_y_kernel(const double* __restrict__ U,
+                                                          const double* UP, int64_t ld,
+                                                          const double* __restrict__ s1,
+                                                          const double* __restrict__ s2, int rows,
+                                                          int cols, double* Y) {
+  const int64_t e = 2 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  if (e >= (int64_t)rows * cols) return;
+  const int i = (int)(e / cols), j = (int)(e - (int64_t)i * cols);
+  const int64_t o = (int64_t)i * ld + j;
+  const double2 u = *reinterpret_cast<const double2*>(U + o);
+  const double a = s1[i];
+  double2 y = {a * u.x, a * u.y};
+  if (UP) {
+    const double2 w = *reinterpret_cast<const double2*>(UP + o);
+    const double b = s2[i];
+    y.x = fma(b, w.x, y.x);
+    y.y = fma(b, w.y, y.y);
+  }
+  *reinterpret_cast<double2*>(Y + o) = y;
+}
+
+hipError_t launch_fitc_grad_y(const double* U, const double* UP, int64_t ld, const double* s1,
+                              const double* s2, int rows, int cols, double* Y, hipStream_t s) {
+  if ((cols & 1) || (ld & 1) || rows <= 0) return hipErrorInvalidValue;
+  const int64_t pairs = (int64_t)rows * cols / 2;
+  hipLaunchKernelGGL(fitc_grad_y_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, U,
+                     UP, ld, s1, s2, rows, cols, Y);
   return hipGetLastError();
 }
 

@@ -75,18 +75,24 @@ def test_fitc_grad_vs_oracle_shapes(gp, n, m, d, iso, obj):
 
 @pytest.mark.parametrize("obj", OBJS)
 def test_fitc_grad_ill_conditioned(gp, obj):
-    """cond(K̃mm) ≈ 1.8e4: the LOO gradients themselves move by up to ~6e-5 (relative) when
-    the inputs are perturbed by 1e-15 relative (1.2e-4 for LogS).  The GPU must agree with the
-    oracle within 10× that measured sensitivity."""
+    """cond(K̃mm) ≈ 1.8e4 (near-duplicate inducing points).  The whitened gradient
+    moves by ~3e-9 under 1e-15 relative input perturbations (the round-3 explicit-inverse form:
+    up to 1.2e-4); the GPU must agree with the oracle, and the GPU's own perturbation floor must
+    stay, under the absolute gradient ceiling fitc_grad_cap = 100·κ·ε."""
+    from conftest import record_floors
+    from test_gpu_parity import fitc_grad_cap
     X, y, Z, th = _shape_case(1000, 37, 3, False, well_conditioned=False)
     val, grad, objs = gp.value_and_grad(th, obj, X=X, y=y, Z=Z)
     ov, og, oz = O.fast_fitc_grad(X, y, Z, *th, obj)
     r = np.random.default_rng(1)
-    pv, pg, pz = O.fast_fitc_grad(X * (1 + 1e-15 * r.standard_normal(X.shape)), y,
-                                  Z * (1 + 1e-15 * r.standard_normal(Z.shape)), *th, obj)
-    sens = max(nrel(pg, og), nrel(pz, oz), 1e-10)
-    assert sens < 1e-3
-    assert nrel(grad, og) <= 10 * sens and nrel(objs["grad_Z"], oz) <= 10 * sens, sens
+    Xp, Zp = X * (1 + 1e-15 * r.standard_normal(X.shape)), Z * (1 + 1e-15 * r.standard_normal(Z.shape))
+    _, pg, pobjs = gp.value_and_grad(th, obj, X=Xp, y=y, Z=Zp)
+    cap = fitc_grad_cap(Z, th)
+    err = {"grad": nrel(grad, og), "grad_Z": nrel(objs["grad_Z"], oz)}
+    floor = {"grad": nrel(pg, grad), "grad_Z": nrel(pobjs["grad_Z"], objs["grad_Z"])}
+    record_floors(f"fitc_grad_ill_{obj}", err, floor, {k: cap for k in err})
+    for k in err:
+        assert max(err[k], floor[k]) <= cap, (k, err[k], floor[k], cap)
 
 
 @pytest.mark.parametrize("obj", OBJS)

@@ -110,18 +110,18 @@ def _floor(X, y, Xt, yt, Z, th, with_grad, gpu_ctx, ref):
     return fl
 
 
-def _compare(parts, ref, floor, cap, test, factor=30.0, abs_min=1e-13):
+def _compare(parts, ref, floor, cap, test, factor=30.0, abs_min=1e-13, grad_cap=None):
     d = _diffs(parts, ref)
-    caps = {k: cap + abs_min for k in d}
+    # absolute ceilings: test_gpu_parity.fitc_cap for the forward outputs, fitc_grad_cap (two
+    # solves deep) for the θ- and Z-gradients — neither the error nor the floor may exceed it
+    gcap = 2.0 * cap if grad_cap is None else grad_cap
+    caps = {k: (gcap if k.startswith("g") else cap) + abs_min for k in d}
     record_floors(test, d, floor, caps)
     for k, v in sorted(d.items()):
         print(f"{k:16s} sharded {v:.2e}  floor {floor[k]:.2e}  cap {caps[k]:.2e}")
     bad = {k: (v, floor[k]) for k, v in d.items() if v > factor * floor[k] + abs_min}
     assert not bad, bad
-    # absolute ceiling (test_gpu_parity.fitc_cap): neither the error nor the floor of a forward
-    # output may exceed it; the gradients (one more solve deep) keep the floor multiple alone
-    over = {k: (v, floor[k], caps[k]) for k, v in d.items()
-            if not k.startswith("g") and max(v, floor[k]) > caps[k]}
+    over = {k: (v, floor[k], caps[k]) for k, v in d.items() if max(v, floor[k]) > caps[k]}
     assert not over, over
 
 
@@ -248,17 +248,15 @@ def test_fitc_blockloo_shards(gpu_ctx, P, nfold, objective):
                     Z=Z * (1 + 1e-15 * rng.standard_normal(Z.shape)))
         for k, v in diffs([gp.block_loo(th, objective, nfold=nfold, grad=True)]).items():
             floor[k] = max(floor.get(k, 0.0), v)
-    from test_gpu_parity import fitc_cap
-    cap = fitc_cap(Z, th)
-    caps = {k: cap + 1e-13 for k in errs}
+    from test_gpu_parity import fitc_cap, fitc_grad_cap
+    cap, gcap = fitc_cap(Z, th), fitc_grad_cap(Z, th)
+    caps = {k: (gcap if k.startswith("grad") else cap) + 1e-13 for k in errs}
     record_floors(f"fitc_blockloo_shards_P{P}_{objective}", errs, floor, caps)
-    print(errs, floor, cap)
+    print(errs, floor, caps)
     bad = {k: (v, floor[k]) for k, v in errs.items() if v > 30.0 * floor[k] + 1e-13}
     assert not bad, bad
-    # absolute ceiling on the objective values (the gradients keep the floor multiple alone,
-    # as in _compare)
-    over = {k: (errs[k], floor[k], caps[k]) for k in ("value", "folds")
-            if max(errs[k], floor[k]) > caps[k]}
+    # absolute ceilings on the values (fitc_cap) and the θ- / Z-gradients (fitc_grad_cap)
+    over = {k: (errs[k], floor[k], caps[k]) for k in errs if max(errs[k], floor[k]) > caps[k]}
     assert not over, over
 
 
