@@ -337,7 +337,15 @@ def cpu_baseline(config="C3"):
         t_fast = time.perf_counter() - t0
     info = RT.host_info()
     info.update(cinfo)
+    scaling = cpu_thread_scaling(RT, cores)
     return {"value": 1.0 / t, "unit": f"fit+predict+score units/s ({config})",
+            "threads_rationale": "threads_used = the lease's host-CPU share: the GPU box presets "
+                                 "OMP_NUM_THREADS to its share of the host (16 per GPU) and its "
+                                 "rules size worker pools to that share, while sched_getaffinity / "
+                                 "os.cpu_count report the whole 256-thread host; threads beyond "
+                                 "the share would run on other jobs' CPUs.  thread_scaling below "
+                                 "measures how the ref-mirror scales up to the share.",
+            "thread_scaling": scaling,
             "cores": cores, "kind": "port", "host": info,
             "sample": f"torch-CPU fp64 ref-mirror of the reference op sequence on the full C3 "
                       f"workload {config} n={c['n']} d={c['d']} n*={c['nt']}, one unit: {t:.1f} s "
@@ -346,6 +354,30 @@ def cpu_baseline(config="C3"):
             "fast_cpu_note": "oracle.fast_full: numpy/LAPACK potrf + L^-1 products on the same unit "
                              f"and {cores} BLAS threads (the GPU's algorithm, not the reference's "
                              "op sequence)"}, ref
+
+
+def cpu_thread_scaling(RT, cores):
+    """The torch-CPU ref-mirror on a quarter-C2 unit (n = 2500, d = 8, n* = 625) at 1, 2, 4, …
+    threads up to the lease's share: the parallel efficiency t(1) / (p·t(p)) shows how the
+    threads_used baseline would move with more host threads (an estimate beyond p, and a
+    conservative one: the C3 unit has 512× this unit's flops to spread)."""
+    import torch
+    n, nt = 2500, 625
+    X, y, Xt, yt, _, th = synth(n, 8, nt, 2)
+    out = {}
+    p = 1
+    while p <= cores:
+        torch.set_num_threads(p)
+        RT.ref_full(X[:256], y[:256], Xt[:64], yt[:64], *th)  # spin the pool up at this width
+        t0 = time.perf_counter()
+        RT.ref_full(X, y, Xt, yt, *th)
+        out[str(p)] = time.perf_counter() - t0
+        p *= 2
+    torch.set_num_threads(cores)
+    t1 = out["1"]
+    return {"workload": f"n={n}, d=8, n*={nt} unit, torch-CPU fp64 ref-mirror",
+            "seconds": out,
+            "efficiency": {k: t1 / (int(k) * v) for k, v in out.items()}}
 
 
 PARITY_VECS = ("loo_mu", "loo_var", "pred_mu", "pred_var")

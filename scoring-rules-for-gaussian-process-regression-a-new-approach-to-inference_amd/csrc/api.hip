@@ -854,23 +854,46 @@ struct EsArgs {
   double diag_ub = 0.0;           // diag(C_f) <= diag_ub, so λmax <= b·diag_ub
 };
 
-// Newton–Schulz steps for a spectrum of C/s inside [x0, 1]: the eigenvalue x of Z_kY_k
-// follows x ← x(3 − x)²/4 (×2.25 per step while small, then quadratic); two more steps let
-// the derivative block of the gradient pass settle
-int ns_iterations(double x0) {
-  double x = std::max(x0, 1e-300);
-  int k = 0;
-  while (1.0 - x > 1e-16 && k < 200) {
-    x = x * (3.0 - x) * (3.0 - x) / 4.0;
-    ++k;
+// Scaled Newton–Schulz schedule for a spectrum of C/s inside [x0, 1] (round 4).  The eigenvalue x
+// of Z_kY_k follows x ← f(x) = x(3 − x)²/4: ×2.25 per step while small (~20 steps from x0 = 8e-6).
+// Scaling the iterates by a scalar keeps the invariant Y_kZ_k⁻¹ = C/s (so the limit is still
+// (C/s)^½) and turns the step into x ← f(βx) with Y ← √β·Y T, Z ← √β·T Z, T = (3I − βZY)/2.
+// With the spectrum known to lie in [l, u], β equalises the images of the two ends,
+// f(βl) = f(βu) (βu < 3: f is increasing to 1 at x = 1 and falls to 0 at 3), which maximises the
+// new lower bound min f(β[l, u]); the new upper bound is 1 once βl ≤ 1 ≤ βu.  The lower bound then
+// grows ×6.7 per step instead of ×2.25: 12 steps instead of 20 from x0 = 8e-6.  Two unscaled
+// steps follow, which let the derivative block of the gradient pass settle.  Returns β per step.
+std::vector<double> ns_schedule(double x0) {
+  auto f = [](double x) { return x * (3.0 - x) * (3.0 - x) / 4.0; };
+  double l = std::min(std::max(x0, 1e-300), 1.0), u = 1.0;
+  std::vector<double> beta;
+  while (1.0 - l > 4e-16 && beta.size() < 200) {
+    double b = 1.0 / u;
+    // scaled while the lower bound is small; from l = 0.5 on the unscaled step converges
+    // quadratically (scaling there only chases rounding in the bounds)
+    if (l < 0.5 && f(b * l) < f(b * u)) {  // bisect f(βl) = f(βu) on [1/u, 2.999/u]
+      double lo = 1.0 / u, hi = 2.999 / u;
+      for (int it = 0; it < 100; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (f(mid * l) < f(mid * u)) lo = mid;
+        else hi = mid;
+      }
+      b = lo;
+    }
+    const double nl = std::min(f(b * l), f(b * u));
+    u = (b * l <= 1.0 && 1.0 <= b * u) ? 1.0 : std::max(f(b * l), f(b * u));
+    l = std::min(nl, u);
+    beta.push_back(b);
   }
-  return k + 2;
+  beta.push_back(1.0);
+  beta.push_back(1.0);
+  return beta;
 }
 
 // Energy score of one fold, ES(m, c, shape1, y, S, β) (KF:70-101) as the scripts call it on
 // the block-LOO predictive (KF:652-655): m − y = −r, C = P_f⁻¹ (PI, full, bp×bp).
-//   R = C^½ by the coupled Newton–Schulz iteration on C/s (T = (3I − ZY)/2, Y ← YT, Z ← TZ:
-//   three b×b MFMA GEMMs per step; the scripts take an SVD, KF:74-77, which has no GEMM form);
+//   R = C^½ by the scaled coupled Newton–Schulz iteration on C/s (T = (3I − βZY)/2,
+//   Y ← √β·YT, Z ← √β·TZ, β per step from ns_schedule: three b×b MFMA GEMMs per step; the scripts take an SVD, KF:74-77, which has no GEMM form);
 //   z = ξR, ẑ = [ξ'R; −r], D_ij = ‖z_i − ẑ_j‖ (es_dist),
 //   ES = (1/S)Σ_i D_iS^β − Σ_{i,j<S} D_ij^β / (2S(S−1)) (es_reduce) → *out (device).
 // With G (ldg): Ḡ = ∂ES/∂R = ξᵀG_z + ξ'ᵀG_ẑ, G_z = diag(ΣW)z − Wẑ, G_ẑ = diag(ΣWᵀ)ẑ − Wᵀz
@@ -887,7 +910,9 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   const int nmat = grad ? 10 : 5;
   const bool bounded = es.lam_lb > 0.0;
   const double sc = bounded ? (double)b * es.diag_ub : trace_c;
-  const int iters = bounded ? ns_iterations(es.lam_lb / sc) : 200;
+  // β per step (ns_schedule); adaptive mode (no spectral bounds) runs unscaled steps
+  const std::vector<double> beta = bounded ? ns_schedule(es.lam_lb / sc) : std::vector<double>(200, 1.0);
+  const int iters = (int)beta.size();
   // with a gradient and a known step count the forward iterates Y_k, Z_k, T_k are kept
   // (3·iters + 2 matrices, < 1 GB at b = 1250) so the derivative pass runs only the
   // 6 products of the off-diagonal blocks per step instead of 9
@@ -953,7 +978,8 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
       Yn = Ys[it + 1];
       Zn = Zk[it + 1];
     }
-    if ((rc = sym(Z, Y, T, -0.5, 0.0))) return rc;
+    const double bt = beta[it], mu = std::sqrt(bt);
+    if ((rc = sym(Z, Y, T, -0.5 * bt, 0.0))) return rc;
     HIPCHK(launch_diag_add_const(T, bp, (int)bp, 1.5, s));
     HIPCHK(mirror(T));
     if (!bounded && extra < 0) {  // ‖T − I‖²_F = ‖I − ZY‖²_F / 4
@@ -962,9 +988,9 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
       HIPCHK(hipStreamSynchronize(s));
       if (ctx->hsmall[0] < 1e-24 * (double)bp) extra = 3;
     }
-    if ((rc = sym(Y, T, Yn, 1.0, 0.0))) return rc;
+    if ((rc = sym(Y, T, Yn, mu, 0.0))) return rc;
     HIPCHK(mirror(Yn));
-    if ((rc = sym(T, Z, Zn, 1.0, 0.0))) return rc;
+    if ((rc = sym(T, Z, Zn, mu, 0.0))) return rc;
     HIPCHK(mirror(Zn));
     std::swap(Y, Yn);
     std::swap(Z, Zn);
@@ -1003,29 +1029,30 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   }
   HIPCHK(launch_ns_init(nullptr, 0, (int)b, (int)bp, 0.0, 0.0, Z2, s));
   for (int it = 0; it < used; ++it) {
+    const double bt = beta[it], mu = std::sqrt(bt);  // the forward step's scaling
     const double *Yk = Y1, *Zkk = Z1, *Tk = T1;
     if (stored) {
       Yk = Ys[it];
       Zkk = Zk[it];
       Tk = Ts[it];
     } else {
-      if ((rc = sym(Z1, Y1, T1, -0.5, 0.0))) return rc;
+      if ((rc = sym(Z1, Y1, T1, -0.5 * bt, 0.0))) return rc;
       HIPCHK(launch_diag_add_const(T1, bp, (int)bp, 1.5, s));
       HIPCHK(mirror(T1));
     }
-    if ((rc = sym(Zkk, Y2, T2, -0.5, 0.0))) return rc;  // T2 = −½(Z1Y2 + Z2Y1)
-    if ((rc = sym(Z2, Yk, T2, -0.5, 1.0))) return rc;
+    if ((rc = sym(Zkk, Y2, T2, -0.5 * bt, 0.0))) return rc;  // T2 = −½β(Z1Y2 + Z2Y1)
+    if ((rc = sym(Z2, Yk, T2, -0.5 * bt, 1.0))) return rc;
     HIPCHK(mirror(T2));
-    if ((rc = sym(Yk, T2, Y2n, 1.0, 0.0))) return rc;   // Y2 ← Y1T2 + Y2T1
-    if ((rc = sym(Y2, Tk, Y2n, 1.0, 1.0))) return rc;
+    if ((rc = sym(Yk, T2, Y2n, mu, 0.0))) return rc;   // Y2 ← √β(Y1T2 + Y2T1)
+    if ((rc = sym(Y2, Tk, Y2n, mu, 1.0))) return rc;
     HIPCHK(mirror(Y2n));
-    if ((rc = sym(Tk, Z2, Z2n, 1.0, 0.0))) return rc;   // Z2 ← T1Z2 + T2Z1
-    if ((rc = sym(T2, Zkk, Z2n, 1.0, 1.0))) return rc;
+    if ((rc = sym(Tk, Z2, Z2n, mu, 0.0))) return rc;   // Z2 ← √β(T1Z2 + T2Z1)
+    if ((rc = sym(T2, Zkk, Z2n, mu, 1.0))) return rc;
     HIPCHK(mirror(Z2n));
     if (!stored) {
-      if ((rc = sym(Y1, T1, Y1n, 1.0, 0.0))) return rc;
+      if ((rc = sym(Y1, T1, Y1n, mu, 0.0))) return rc;
       HIPCHK(mirror(Y1n));
-      if ((rc = sym(T1, Z1, Z1n, 1.0, 0.0))) return rc;
+      if ((rc = sym(T1, Z1, Z1n, mu, 0.0))) return rc;
       HIPCHK(mirror(Z1n));
       std::swap(Y1, Y1n);
       std::swap(Z1, Z1n);

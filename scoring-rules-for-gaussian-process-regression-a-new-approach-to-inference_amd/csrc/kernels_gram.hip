@@ -26,6 +26,7 @@ template <int D>
 __global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
   __shared__ __attribute__((aligned(16))) double xs_col[(D ? D : GPS_MAX_D) * GR_COLS];
   __shared__ double xs_row[GR_ROWS * (D ? D : GPS_MAX_D)];
+  __shared__ double2 etab[64];
   const int d = D ? D : p.d;
   const int tiles_x = p.N / GR_COLS;
   const int bx = blockIdx.x % tiles_x;
@@ -44,6 +45,7 @@ __global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
     const int gi = r0 + i;
     xs_row[i * d + k] = gi < p.n ? p.x[(int64_t)gi * d + k] * p.inv_ell[k] : 0.0;
   }
+  exp_tab_stage(etab);
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6;
@@ -73,8 +75,8 @@ __global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
         a1 = fma(e1, e1, a1);
       }
     }
-    double v0 = p.sf2 * exp(-0.5 * a0);
-    double v1 = p.sf2 * exp(-0.5 * a1);
+    double v0 = p.sf2 * exp_neg(-0.5 * a0, etab);
+    double v1 = p.sf2 * exp_neg(-0.5 * a1, etab);
     const bool rowpad = gi >= p.n;
     if (gi == gj) v0 += p.diag_add;
     if (gi == gj + 1) v1 += p.diag_add;
@@ -101,6 +103,7 @@ constexpr int G2_ROWS = 128;
 template <int D>
 __global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
   __shared__ __attribute__((aligned(16))) double xs_row[G2_ROWS * D];
+  __shared__ double2 etab[64];
   const int tiles_x = p.N / GR_COLS;
   const int bx = blockIdx.x % tiles_x;
   const int by = blockIdx.x / tiles_x;
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
     f0[k] = colpad0 ? 0.0 : p.xp[(int64_t)gj * D + k] * p.inv_ell[k];
     f1[k] = colpad1 ? 0.0 : p.xp[(int64_t)(gj + 1) * D + k] * p.inv_ell[k];
   }
+  exp_tab_stage(etab);
   __syncthreads();
 
   // squared scaled distances of row rr to this lane's two columns
@@ -162,7 +166,14 @@ __global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
       double a0, a1;
       dist2(rr, a0, a1);
       double* dst = p.out + (int64_t)(r0 + rr) * p.ldo + gj;
-      *reinterpret_cast<double2*>(dst) = make_double2(p.sf2 * exp(-0.5 * a0), p.sf2 * exp(-0.5 * a1));
+#ifdef GPS_GRAM_NT
+      typedef double nv2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store((nv2){p.sf2 * exp_neg(-0.5 * a0, etab), p.sf2 * exp_neg(-0.5 * a1, etab)},
+                                  reinterpret_cast<nv2*>(dst));
+#else
+      *reinterpret_cast<double2*>(dst) =
+          make_double2(p.sf2 * exp_neg(-0.5 * a0, etab), p.sf2 * exp_neg(-0.5 * a1, etab));
+#endif
     }
     return;
   }
@@ -172,8 +183,8 @@ __global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
     const int gi = r0 + rr;
     double a0, a1;
     dist2(rr, a0, a1);
-    double v0 = p.sf2 * exp(-0.5 * a0);
-    double v1 = p.sf2 * exp(-0.5 * a1);
+    double v0 = p.sf2 * exp_neg(-0.5 * a0, etab);
+    double v1 = p.sf2 * exp_neg(-0.5 * a1, etab);
     const bool rowpad = gi >= p.n;
     if (gi == gj) v0 += p.diag_add;
     if (gi == gj + 1) v1 += p.diag_add;

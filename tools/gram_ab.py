@@ -1,0 +1,36 @@
+"""Gram kernel timings (gram_kff / gram_ksf at C3, gram_knm at C5) of the library this process
+loads (GPSCORE_LIB selects a variant build): hipEvent records over 5 fits, single stream."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd"))
+import bench  # noqa: E402
+import gpscore  # noqa: E402
+
+ctx = gpscore.Context(0)
+out = {"lib": os.environ.get("GPSCORE_LIB", "in-tree")}
+for cfg in ("C3", "C5"):
+    c = bench.CONFIGS[cfg]
+    X, y, Xt, yt, Z, th = bench.synth(c["n"], c["d"], c["nt"], c["seed"], c.get("m"))
+    gp = gpscore.GP(ctx=ctx)
+    if Z is None:
+        gp.set_data(X, y)
+    else:
+        gp.set_data(X, y, kind="fitc", Z=Z)
+    gp.set_test(Xt, yt)
+    gp.fit(theta=th, return_loo=False)
+    ctx.set_overlap(False)
+    ctx.prof(True)
+    for _ in range(5):
+        gp.fit(theta=th, return_loo=False)
+        gp.predict()
+    rep = ctx.prof_collect()
+    ctx.prof(False)
+    ctx.set_overlap(True)
+    for k, v in rep.items():
+        if k.startswith("gram"):
+            out[f"{cfg}.{k}"] = {"ms": v["ms"] / v["count"], "GB/s": v["bytes"] / (v["ms"] * 1e-3) / 1e9}
+print(json.dumps(out))
