@@ -186,6 +186,7 @@ __global__ __launch_bounds__(256) void fitc_grad_contract_kernel(FitcContractPar
   extern __shared__ double xs[];  // [64 cols][d] scaled column features (D == 0 path)
   __shared__ double sh[(1 + FG_DP) * 16];
   __shared__ double zsh[4][FG_COLS][FG_DP + 1];
+  __shared__ double2 etab[64];
   const int d = D > 0 ? D : p.d;
   const int d0 = blockIdx.z * FG_DP;
   const int cj = threadIdx.x & 63, rg = threadIdx.x >> 6;
@@ -196,8 +197,9 @@ __global__ __launch_bounds__(256) void fitc_grad_contract_kernel(FitcContractPar
       const int q = e / d, k = e - q * d, jj = blockIdx.x * FG_COLS + q;
       xs[e] = jj < p.nc ? p.xc[(int64_t)jj * d + k] * p.inv_ell[k] : 0.0;
     }
-    __syncthreads();
   }
+  exp_tab_stage(etab);
+  __syncthreads();
   double xj[D > 0 ? D : 1];
   if constexpr (D > 0) {
 #pragma unroll
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(256) void fitc_grad_contract_kernel(FitcContractPar
             r2 = fma(tk, tk, r2);
           }
         }
-        const double Kij = p.sf2 * exp(-0.5 * r2);
+        const double Kij = p.sf2 * exp_neg(-0.5 * r2, etab);
         double G = 0.0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {

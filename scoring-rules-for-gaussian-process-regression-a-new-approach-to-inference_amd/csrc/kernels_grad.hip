@@ -107,6 +107,7 @@ template <int D>
 __global__ __launch_bounds__(256) void grad_contract_kernel(GradParams p) {
   extern __shared__ double xs[];  // [GT rows][d] then [GT cols][d]
   __shared__ double sh[(2 + DP) * 16];
+  __shared__ double2 etab[64];
   const int d = D > 0 ? D : p.d;
   const int b = blockIdx.x, pass = blockIdx.y, d0 = pass * DP;
   int ti = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
@@ -121,6 +122,7 @@ __global__ __launch_bounds__(256) void grad_contract_kernel(GradParams p) {
     xr[e] = row0 + q < p.n ? p.x[(int64_t)(row0 + q) * d + k] * p.inv_ell[k] : 0.0;
     xc[e] = col0 + q < p.n ? p.x[(int64_t)(col0 + q) * d + k] * p.inv_ell[k] : 0.0;
   }
+  exp_tab_stage(etab);
   __syncthreads();
   const int cj = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int j = col0 + cj;
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void grad_contract_kernel(GradParams p) {
             r2 = fma(t, t, r2);
           }
         }
-        const double K = p.sf2 * exp(-0.5 * r2);
+        const double K = p.sf2 * exp_neg(-0.5 * r2, etab);
         const double ai = p.alpha[i];
         double m = p.a1 * ai * aj;
         if (p.a0 != 0.0) m = fma(p.a0, ldA[u], m);
