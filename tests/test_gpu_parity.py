@@ -251,12 +251,14 @@ def fitc_cap(Z, th):
     return 50.0 * kappa * np.finfo(np.float64).eps
 
 
-def fitc_grad_cap(Z, th):
+def fitc_grad_cap(Z, th, depth=2):
     """Absolute ceiling for the FITC θ- and Z-gradients (normwise relative): 50·κ·ε per solve
-    through C = Q + Λ, two deep (M = a·C⁻¹ − ½(vαᵀ + αvᵀ) − C⁻¹diag(h)C⁻¹).  The whitened
-    gradient (round 4) moves by 16-33·κ·ε under 1e-15 input perturbations on the
-    ill-conditioned cases; the round-3 explicit-inverse form moved by up to 1e6·κ·ε."""
-    return 2.0 * fitc_cap(Z, th)
+    through C = Q + Λ, `depth` deep — 2 for the LOO / NLML gradients (M = a·C⁻¹ − ½(vαᵀ + αvᵀ) −
+    C⁻¹diag(h)C⁻¹), 4 for block-LOO (the rows of C⁻¹, the fold inverse P_f⁻¹ in ∂obj/∂P_f, then
+    M = −C⁻¹GblkC⁻¹).  The whitened gradient (round 4) moves by 16-33·κ·ε (CPU) under
+    1e-15 input perturbations on the ill-conditioned cases; the round-3 explicit-inverse form
+    moved by up to 1e6·κ·ε."""
+    return depth * fitc_cap(Z, th)
 
 
 def test_c1_config_vs_torch_ref(gp):

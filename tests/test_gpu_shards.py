@@ -249,7 +249,7 @@ def test_fitc_blockloo_shards(gpu_ctx, P, nfold, objective):
         for k, v in diffs([gp.block_loo(th, objective, nfold=nfold, grad=True)]).items():
             floor[k] = max(floor.get(k, 0.0), v)
     from test_gpu_parity import fitc_cap, fitc_grad_cap
-    cap, gcap = fitc_cap(Z, th), fitc_grad_cap(Z, th)
+    cap, gcap = fitc_cap(Z, th), fitc_grad_cap(Z, th, depth=4)  # block-LOO: 4 solves deep
     caps = {k: (gcap if k.startswith("grad") else cap) + 1e-13 for k in errs}
     record_floors(f"fitc_blockloo_shards_P{P}_{objective}", errs, floor, caps)
     print(errs, floor, caps)
