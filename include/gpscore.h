@@ -111,6 +111,9 @@ enum {
                              m×m factorisations (the test pre-pass runs beside them) */
   GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
                              flight per load group (2, 3 (default) or 4).  Same values bitwise. */
+  GPS_OPT_GEMM_GLDS = 21, /* 1: 128-tile GEMM launches stage their operands global -> LDS directly
+                             (global_load_lds) instead of through registers; 0 (default).  Same
+                             values bitwise.  Process-wide. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

@@ -82,6 +82,7 @@ GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 extern int g_stream_k;   // 1: the stream-K tail of uniform-K 128-tile launches (launch_gemm)
+extern int g_gemm_glds;  // 1: 128-tile launches stage operands global -> LDS directly (glds)
 constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)
 
 // ------------------------------------------------------------ device reductions

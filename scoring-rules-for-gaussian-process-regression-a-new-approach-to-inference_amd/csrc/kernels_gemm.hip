@@ -125,14 +125,14 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <int ALAY, int BLAY, int EPI, int TILE>
+template <int ALAY, int BLAY, int EPI, int TILE, bool GL = false>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o = -1, int ke_o = -1,
                                           double* part = nullptr);
 template <int ALAY, int BLAY>
 __device__ void gemm_sk_block(const GemmParams& p, int s, double* smem);
 
-template <int ALAY, int BLAY, int EPI, int TILE>
+template <int ALAY, int BLAY, int EPI, int TILE, bool GL>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   const int nblk = p.sk_wgs > 0 ? p.sk_dp : (int)gridDim.x;
   int ti, tj;
   if (!tile_of(p, remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x, ti, tj)) return;
-  gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, blockIdx.y, smem);
+  gemm_tile<ALAY, BLAY, EPI, TILE, GL>(p, ti, tj, blockIdx.y, smem);
 }
 
 // EPI_STORE epilogue: C = alpha·acc (+ beta·C) for this thread's accumulators
@@ -255,7 +255,7 @@ __device__ void gemm_sk_block(const GemmParams& p, int s, double* smem) {
   }
 }
 
-template <int ALAY, int BLAY, int EPI, int TILE>
+template <int ALAY, int BLAY, int EPI, int TILE, bool GL>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o, int ke_o, double* part) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
@@ -411,7 +411,78 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     }
   };
 
-  if (nk > 0) {
+  if constexpr (GL) {
+    // ---- direct global -> LDS staging (GPS_OPT_GEMM_GLDS): global_load_lds_dwordx4, no
+    // staging registers and no ds_write pass.  One wave instruction lands 1 KB contiguously
+    // (lane l at base + 16 l), so i-major sources ([i][k]: A with LAY_N, B with LAY_T) get an
+    // unpadded i-major image — 16-double rows, 16-byte chunk c of row r stored at chunk
+    // c ^ ((r >> 1) & 7) (the permutation goes on the SOURCE address, cdna_hip_programming.md
+    // rule 21), which makes the fragment reads (16 rows, one k) conflict-free — and k-major
+    // sources keep the padded k-major image (each wave instruction is exactly one 1-KB k row).
+    // Fragments take the same k order as the register path: bitwise the same products.
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+    auto glds_imaj = [&](const double* src, int64_t ld, int base, int k0, double* img) {
+#pragma unroll
+      for (int q = 0; q < TILE / 32; ++q) {  // rows 32·wave + 8q .. +8, one instruction each
+        const int r0 = (TILE / 4) * wave + 8 * q, r = r0 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (int64_t)(base + r) * ld + k0 + 2 * c),
+                                         (lds_ptr_t)(img + r0 * BK), 16, 0, 0);
+      }
+    };
+    auto glds_kmaj = [&](const double* src, int64_t ld, int base, int k0, double* img) {
+#pragma unroll
+      for (int q = 0; q < BK / 4; ++q) {  // k rows 4·wave + q (TILE = 128: one instruction each)
+        const int k = (BK / 4) * wave + q;
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (int64_t)(k0 + k) * ld + base + 2 * lane),
+                                         (lds_ptr_t)(img + k * LS), 16, 0, 0);
+      }
+    };
+    auto stage = [&](int buf, int k0) {
+      double* As = smem + buf * STAGE;
+      double* Bs = As + BK * LS;
+      if constexpr (ALAY == LAY_N) glds_imaj(p.A, p.lda, row0, k0, As);
+      else glds_kmaj(p.A, p.lda, row0, k0, As);
+      if constexpr (BLAY == LAY_T) glds_imaj(p.B, p.ldb, col0, k0, Bs);
+      else glds_kmaj(p.B, p.ldb, col0, k0, Bs);
+    };
+    auto frag = [&](const double* img, bool imaj, int r, int k) {
+      return imaj ? img[r * BK + 2 * ((k >> 1) ^ ((r >> 1) & 7)) + (k & 1)] : img[k * LS + r];
+    };
+    auto compute_gl = [&](int buf) {
+      const double* As = smem + buf * STAGE;
+      const double* Bs = As + BK * LS;
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        const int k = kk * 4 + (lane >> 4);
+        double a[MI], b[MI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) a[mi] = frag(As, ALAY == LAY_N, wr * WT + mi * 16 + (lane & 15), k);
+#pragma unroll
+        for (int ni = 0; ni < MI; ++ni) b[ni] = frag(Bs, BLAY == LAY_T, wc * WT + ni * 16 + (lane & 15), k);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < MI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      }
+    };
+    if (nk > 0) {
+      stage(0, kb);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      // steady state: slice it+1's loads go out before slice it is multiplied; each wave waits
+      // for its own DMA, then the barrier publishes every wave's (MI355X_MICROARCH item 7)
+      for (int it = 0; it < nk - 1; ++it) {
+        stage((it + 1) & 1, kb + (it + 1) * BK);
+        compute_gl(it & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      compute_gl((nk - 1) & 1);
+    }
+  } else if (nk > 0) {
     load_tile(kb);
     store_tile(0);
     __syncthreads();
@@ -682,6 +753,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 }
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
+int g_gemm_glds = 0;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
 int g_stream_k = 0;   // GPS_OPT_STREAM_K (process-wide; off: DESIGN §6.20)
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
@@ -818,10 +890,16 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   }
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
-#define GPS_GEMM_CASE(AL, BL, EP, T)                                               \
-  if (err == hipErrorInvalidValue && alay == AL && blay == BL && epi == EP && tile == T) { \
-    hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T>), grid, block, 0, s, q);   \
-    err = hipGetLastError();                                                       \
+  // direct-to-LDS staging (GPS_OPT_GEMM_GLDS): 128-tiles without a per-k operand scale, the
+  // stream-K tail, or the row-dot epilogue (which reads the k-major A image)
+  const bool gl = g_gemm_glds && tile == 128 && !q.kscale && q.sk_wgs == 0 && epi != EPI_ROWSQ_DOT;
+#define GPS_GEMM_CASE(AL, BL, EP, T)                                                          \
+  if (err == hipErrorInvalidValue && alay == AL && blay == BL && epi == EP && tile == T) {   \
+    if (T == 128 && gl)                                                                       \
+      hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T, (T == 128)>), grid, block, 0, s, q); \
+    else                                                                                      \
+      hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T, false>), grid, block, 0, s, q);    \
+    err = hipGetLastError();                                                                  \
   }
   GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE, 128)
   GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE, 128)

@@ -799,3 +799,39 @@ def test_persistent_factorisation_potrf_exports(gpu_ctx):
     with pytest.raises(gpscore.NotPositiveDefinite) as ei:
         compat.half_logdet(Abad)
     assert ei.value.info == 1501
+
+
+def test_gemm_glds_bitwise(gpu_ctx):
+    """GPS_OPT_GEMM_GLDS (direct global -> LDS operand staging in the 128-tile GEMM)
+    computes every product with the same fragments in the same k order as register staging: the
+    full-GP fit + predict (NT / NN / TN products, SYRKs, the fused predictive column reductions)
+    and the FITC fit + predict + gradient (row-norm epilogues, Woodbury products) are bitwise
+    the same either way."""
+    import gpscore
+    rng = np.random.default_rng(21)
+    X, Xt = rng.standard_normal((5000, 6)), rng.standard_normal((1500, 6))
+    y, yt = np.sin(X.sum(1)), np.sin(Xt.sum(1))
+    Z = X[rng.choice(5000, 700, replace=False)]
+    th = (0.0, np.log(1.5), np.log(0.02))
+
+    def run():
+        gp = gpscore.GP(ctx=gpu_ctx)
+        r = gp.fit(X, y, th)
+        mu, var = gp.predict(Xt, yt)
+        gf = gpscore.GP(ctx=gpu_ctx)
+        gf.set_data(X, y, kind="fitc", Z=Z)
+        gf.set_test(Xt, yt)
+        rf = gf.fit(theta=th)
+        muf, varf = gf.predict()
+        _, g, objs = gf.value_and_grad(th, "loo_crps")
+        return [r.mu_loo, r.var_loo, mu, var, rf.mu_loo, rf.var_loo, muf, varf, g, objs["grad_Z"],
+                np.array(list(r.objectives.values()) + list(rf.objectives.values()))]
+
+    base = run()
+    try:
+        gpu_ctx.call("gps_ctx_set_option", 21, 1)
+        gl = run()
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", 21, 0)
+    for a, b in zip(gl, base):
+        assert np.array_equal(a, b)
