@@ -111,6 +111,10 @@ enum {
                              m×m factorisations (the test pre-pass runs beside them) */
   GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
                              flight per load group (2, 3 (default) or 4).  Same values bitwise. */
+  GPS_OPT_DAG_FINE = 22,  /* 1 (default): the persistent factorisation runs the leaf chain's TRSM and
+                             diagonal update as fine parts (16×16 blocks per wave, 8 / 16 workgroups
+                             per tile); 0: as 4 row strips like every other tile task.  Same values
+                             (the strips add exact zero products above X_kk's diagonal). */
   GPS_OPT_GEMM_GLDS = 21, /* 1: 128-tile GEMM launches stage their operands global -> LDS directly
                              (global_load_lds) instead of through registers; 0 (default).  Same
                              values bitwise.  Process-wide. */
@@ -131,10 +135,10 @@ enum { GPS_STAT_GRAPHS = 0, GPS_STAT_GRAPH_CAP = 1, GPS_STAT_GRAPH_OVERFLOW = 2,
 int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
 
 /* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one
- * word per strip task (type | part << 3 | i << 8 | j << 16 | k << 24; types 0 LEAF, 1 TRSM,
- * 2 UPD, 3 UPDX, 4 FIN — kernels_potrf.hip).  Returns the queue length (writes at most cap
- * words); needs no device. */
-int gps_dag_task_list(int T, uint32_t* out, int cap);
+ * word per strip task (type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24; types 0 LEAF,
+ * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN; fine: the chain tasks' parts as GPS_OPT_DAG_FINE —
+ * kernels_potrf.hip).  Returns the queue length (writes at most cap words); needs no device. */
+int gps_dag_task_list(int T, int fine, uint32_t* out, int cap);
 
 /* on: 0 off, 1 per-kernel-class tags, 2 GEMM tags also carry layout/shape/tri/split-K/lda */
 int gps_prof_enable(gps_ctx* ctx, int on);

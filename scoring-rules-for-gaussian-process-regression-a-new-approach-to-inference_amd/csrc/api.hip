@@ -105,8 +105,9 @@ struct gps_ctx {
   int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
   int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: automatic, see dag_width)
+  bool dag_fine = true;                // GPS_OPT_DAG_FINE
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
-  std::map<int, std::pair<DBuf, int>> dag_lists;  // per block size T: device task list, length
+  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2T + fine: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
   int64_t dag_cnt_used = 0;
@@ -477,7 +478,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     return 0;
   }
   if (dag_block(ctx, nb)) {  // the whole block in one persistent launch (kernels_potrf.hip)
-    auto it = ctx->dag_lists.find(nb);
+    auto it = ctx->dag_lists.find(2 * nb + ctx->dag_fine);
     const int64_t need = dag_cnt_ints(nb);
     if (it == ctx->dag_lists.end() || ctx->dag_cnt_used + need > (int64_t)(ctx->dag_cnt.cap / 4))
       return fail(ctx, -2, "persistent factorisation: task list / counters not prepared");
@@ -610,9 +611,10 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   int64_t dcnt = 0;
   dag_blocks(ctx, n_pad / GPS_TILE, dsizes, dcnt);
   for (int T : dsizes) {
-    if (ctx->dag_lists.count(T)) continue;
-    const std::vector<uint32_t> tl = dag_task_list(T);
-    auto& e = ctx->dag_lists[T];
+    const int lk = 2 * T + ctx->dag_fine;
+    if (ctx->dag_lists.count(lk)) continue;
+    const std::vector<uint32_t> tl = dag_task_list(T, 1, ctx->dag_fine);
+    auto& e = ctx->dag_lists[lk];
     HIPCHK(ensure(ctx, e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
     // capturing a graph on its own thread, and a legacy-stream call then fails)
@@ -651,7 +653,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
       (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_half,
       (uintptr_t)ctx->dag_cnt.p, (uintptr_t)ctx->sk_cnt.p};
-  for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[T].first.p);  // the task lists
+  for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[2 * T + ctx->dag_fine].first.p);  // the task lists
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       g.last_use = ++ctx->graph_tick;
@@ -1344,6 +1346,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ARGCHK(value >= 0, "GPS_OPT_DAG_WGS must be >= 0");
       ctx->dag_wgs = value;
       return 0;
+    case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
     case GPS_OPT_DAG_GROUP:
       ARGCHK(value >= 2 && value <= 4, "GPS_OPT_DAG_GROUP must be 2, 3 or 4");
       ctx->dag_group = value;
@@ -1378,9 +1381,9 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
   return 0;
 }
 
-int gps_dag_task_list(int T, uint32_t* out, int cap) {
+int gps_dag_task_list(int T, int fine, uint32_t* out, int cap) {
   if (T < 2 || T > 64 || cap < 0 || (cap > 0 && !out)) return fail(nullptr, -1, "bad arguments");
-  const std::vector<uint32_t> tl = dag_task_list(T);
+  const std::vector<uint32_t> tl = dag_task_list(T, 1, fine != 0);
   for (int i = 0; i < cap && i < (int)tl.size(); ++i) out[i] = tl[i];
   return (int)tl.size();
 }

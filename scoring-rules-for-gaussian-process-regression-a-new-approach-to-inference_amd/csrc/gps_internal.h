@@ -242,7 +242,7 @@ hipError_t launch_potrf_leaf(const double* A, int64_t lda, double* Linv, int64_t
 // persistent tiled factorisation of a diagonal block of T tiles (kernels_potrf.hip): L⁻¹ into
 // Linv, L into A's strictly-lower tiles (and Lout if given), logdiag, info[0] as the leaf;
 // info[1] != 0x7f7f7f7f on a lost dependency (bounded spin).  cnt: 16 + 2·T² ints, zero at the
-// launch and left zero by it (its last workgroup resets them); tasks: dag_task_list(T) on the device.
+// launch and left zero by it (its last workgroup resets them); tasks: dag_task_list(T, ..) on the device.
 struct DagParams {
   double* A; int64_t lda;
   double* Linv; int64_t ldl;
@@ -256,7 +256,7 @@ struct DagParams {
   int group = 3;                   // 16-deep operand chunks per load group of a strip task (2..4)
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
-std::vector<uint32_t> dag_task_list(int T, int order = 1);
+std::vector<uint32_t> dag_task_list(int T, int order = 1, bool fine = true);
 inline int64_t dag_cnt_ints(int T) { return (16 + 2 * (int64_t)T * T + 63) / 64 * 64; }
 
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)

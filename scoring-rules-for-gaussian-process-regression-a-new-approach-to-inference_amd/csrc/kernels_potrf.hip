@@ -436,6 +436,9 @@ using v4::dv2;
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 constexpr int NP = 4;        // strips per tile task
+constexpr int NPF_TRSM = 8;  // parts of a fine TRSM (16-row strips)
+constexpr int NPF_UPD = 16;  // parts of a fine UPD (16 × 64 blocks)
+constexpr int U = 16;        // arrivals per finished tile task: 4 per strip, 2 / 1 per fine part
 constexpr int AUX_SC1 = 16;  // cache-policy bits of the buffer intrinsics: sc1
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* base, uint32_t bytes) {
@@ -571,6 +574,95 @@ __device__ __forceinline__ void run_strip(const Strip& s) {
       }
 }
 
+// Fine parts of the two tile tasks on the leaf chain, TRSM(k+1,k) and UPD(k+1,k+1,k) (round 4):
+// LEAF(k) -> TRSM(k+1,k) -> UPD(k+1,k+1,k) -> LEAF(k+1) ran 9.5 + 11.7 µs of strip tasks per
+// 128 columns (profiles/r3_dag_trace20_rank.txt), each wave a 32×32 block with K = 128: 128
+// dependent-group MFMAs (3.4 µs) behind several fabric round trips.  A fine part gives each wave
+// 16×16 blocks (TRSM: 16 rows, the column blocks w and 7 − w, whose triangular K ranges sum to
+// the same 144; UPD: one block), every operand chunk in flight before the first MFMA.  The
+// in-place TRSM keeps whole rows per workgroup (its A strip is read across all columns).  The
+// MFMA sequence per output element is the strip task's (chunks ascending, the same k
+// permutation): the same bits, bar the all-zero chunks above X_kk's diagonal the strip adds.
+// one wave: acc[c] = A (16 rows, k < ke[c]) · B_cᵀ (B_c: 16 rows, [j][k]), c < 2, ke ≤ 128
+__device__ __forceinline__ void wave_gemm16(const double* Ap, int64_t lda, const double* B0,
+                                            const double* B1, int64_t ldb, int ke0, int ke1,
+                                            d4 (&acc)[2]) {
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(Ap, (uint32_t)(16 * lda * 8));
+  const __amdgpu_buffer_rsrc_t rb0 = rsrc(B0, (uint32_t)(16 * ldb * 8));
+  const __amdgpu_buffer_rsrc_t rb1 = rsrc(B1 ? B1 : B0, (uint32_t)(16 * ldb * 8));
+  const int kmax = ke0 > ke1 ? ke0 : ke1;
+  double a[8][4], b0[8][4], b1[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int k = 16 * u + 4 * g;
+    const uint32_t o = (uint32_t)(((int64_t)r * lda + k) * 8), ob = (uint32_t)(((int64_t)r * ldb + k) * 8);
+    if (16 * u < kmax) {
+      const dv2 x0 = ld128(ra, o), x1 = ld128(ra, o + 16);
+      a[u][0] = x0.x; a[u][1] = x0.y; a[u][2] = x1.x; a[u][3] = x1.y;
+    }
+    if (16 * u < ke0) {
+      const dv2 x0 = ld128(rb0, ob), x1 = ld128(rb0, ob + 16);
+      b0[u][0] = x0.x; b0[u][1] = x0.y; b0[u][2] = x1.x; b0[u][3] = x1.y;
+    }
+    if (16 * u < ke1) {
+      const dv2 x0 = ld128(rb1, ob), x1 = ld128(rb1, ob + 16);
+      b1[u][0] = x0.x; b1[u][1] = x0.y; b1[u][2] = x1.x; b1[u][3] = x1.y;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (16 * u < ke0) acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][kk], b0[u][kk], acc[0], 0, 0, 0);
+      if (16 * u < ke1) acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][kk], b1[u][kk], acc[1], 0, 0, 0);
+    }
+}
+
+// one fine part on all four waves: each wave's (up to) two 16×16 output blocks of C rows
+// [0, 16), columns c0·16.. and c1·16.. (c < 0: none); barrier before the write-through stores
+// (the TRSM reads its strip in place)
+struct Fine {
+  const double* A; int64_t lda;      // the strip's 16 rows, k from 0
+  const double* B; int64_t ldb;      // B block c at B + 16c·ldb (rows [j][k])
+  double* C; int64_t ldc;            // C block c at C + 16c
+  double* C2; int64_t ldc2;          // optional plain copy (L into Lout)
+  double alpha, beta;
+  int c0, c1, ke0, ke1;              // per wave
+};
+__device__ __forceinline__ void run_fine(const Fine& s) {
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  d4 acc[2] = {(d4){0.0, 0.0, 0.0, 0.0}, (d4){0.0, 0.0, 0.0, 0.0}};
+  const int cs[2] = {s.c0, s.c1};
+  double cold[2][4];
+  const __amdgpu_buffer_rsrc_t rc = rsrc(s.C, (uint32_t)(16 * s.ldc * 8));
+  if (s.beta != 0.0) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (cs[c] >= 0)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          cold[c][e] = ld64(rc, (uint32_t)(((int64_t)(g + 4 * e) * s.ldc + 16 * cs[c] + r) * 8));
+  }
+  const int ke0 = s.c0 >= 0 ? s.ke0 : 0, ke1 = s.c1 >= 0 ? s.ke1 : 0;
+  if (ke0 | ke1)
+    wave_gemm16(s.A, s.lda, s.B + (int64_t)16 * (s.c0 >= 0 ? s.c0 : 0) * s.ldb,
+                s.c1 >= 0 ? s.B + (int64_t)16 * s.c1 * s.ldb : nullptr, s.ldb, ke0, ke1, acc);
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (cs[c] < 0) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      double v = s.alpha * acc[c][e];
+      if (s.beta != 0.0) v = fma(s.beta, cold[c][e], v);
+      const int64_t row = g + 4 * e, col = 16 * cs[c] + r;
+      st64(rc, (uint32_t)((row * s.ldc + col) * 8), v);
+      if (s.C2) s.C2[row * s.ldc2 + col] = v;
+    }
+  }
+}
+
 // Counters: cnt[0] the queue head, cnt[1] the workgroups out, cnt[16..] the arrival counters —
 // zero at launch, zero again when the last workgroup leaves.
 // TRACE: per queue slot t, trace[4t..4t+3] = {fetched, inputs ready, outputs drained} in 100 MHz
@@ -596,6 +688,7 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
   // that only lane 0 takes, and the SIMT lowering then loops the other lanes over a stale task.
   int* out = nullptr;
   int* out2 = nullptr;
+  int inc = 0;                         // the arrival the current task adds to *out
   unsigned long long* trow = nullptr;  // TRACE: the current slot's record
   int ndone = 0;                       // queue slots this workgroup completed
   for (;;) {
@@ -603,7 +696,7 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
       if constexpr (TRACE) {  // (the previous task's "done" stamp lives here for the same reason)
         if (trow) trow[2] = __builtin_amdgcn_s_memrealtime();
       }
-      if (out) __hip_atomic_fetch_add(out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (out) __hip_atomic_fetch_add(out, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (out2) __hip_atomic_fetch_add(out2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int t = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sh[0] = t < p.ntasks ? p.tasks[t] : 0xffffffffu;
@@ -622,8 +715,8 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
         trow[3] = (unsigned long long)blockIdx.x << 8 | (xcc & 15);
       }
     }
-    const int type = w & 7, part = (w >> 3) & 3, ti = (w >> 8) & 255, tj = (w >> 16) & 255,
-              tk = (w >> 24) & 255;
+    const int type = w & 7, part = (w >> 3) & 15, fine = (w >> 7) & 1, ti = (w >> 8) & 255,
+              tj = (w >> 16) & 255, tk = (w >> 24) & 255;
     // ---- the counts this task needs (see the header); up to three, polled by wave 0 (every
     //      lane loads the same word; the exit test is taken on lane 0's view)
     if (wave == 0) {
@@ -631,24 +724,24 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
       int v0 = 0, v1 = 0, v2 = 0;
       switch (type) {
         case 0:  // LEAF(k = ti)
-          c0 = acnt + ti * T + ti; v0 = NP * ti;
+          c0 = acnt + ti * T + ti; v0 = U * ti;
           break;
         case 1:  // TRSM(i, k)
-          c0 = acnt + ti * T + tk; v0 = NP * tk;
-          c1 = acnt + tk * T + tk; v1 = NP * tk + 1;
+          c0 = acnt + ti * T + tk; v0 = U * tk;
+          c1 = acnt + tk * T + tk; v1 = U * tk + 1;
           break;
         case 2:  // UPD(i, j, k)
-          c0 = acnt + ti * T + tk; v0 = NP * (tk + 1);
-          c1 = acnt + tj * T + tk; v1 = NP * (tk + 1);
-          c2 = acnt + ti * T + tj; v2 = NP * tk;
+          c0 = acnt + ti * T + tk; v0 = U * (tk + 1);
+          c1 = acnt + tj * T + tk; v1 = U * (tk + 1);
+          c2 = acnt + ti * T + tj; v2 = U * tk;
           break;
         case 3:  // UPDX(i, k, j): L_ij final, X_jk final, S_ik's earlier terms
-          c0 = acnt + ti * T + tj; v0 = NP * (tj + 1);
-          c1 = xcnt + tj * T + tk; v1 = tj == tk ? 1 : NP * (tj - tk + 1);
-          c2 = xcnt + ti * T + tk; v2 = NP * (tj - tk);
+          c0 = acnt + ti * T + tj; v0 = U * (tj + 1);
+          c1 = xcnt + tj * T + tk; v1 = tj == tk ? 1 : U * (tj - tk + 1);
+          c2 = xcnt + ti * T + tk; v2 = U * (tj - tk);
           break;
         default:  // FIN(i, k)
-          c0 = xcnt + ti * T + tk; v0 = NP * (ti - tk);
+          c0 = xcnt + ti * T + tk; v0 = U * (ti - tk);
           c1 = xcnt + ti * T + ti; v1 = 1;
           break;
       }
@@ -699,7 +792,35 @@ __global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
                           p.info, p.base + (int)o, p.nreal - (int)o, S, DG);
       out = acnt + ti * T + ti;
       out2 = xcnt + ti * T + ti;
+      inc = 1;
+    } else if (fine) {
+      Fine f;
+      const int64_t R = 128 * (int64_t)ti, K = 128 * (int64_t)tk;
+      f.C2 = nullptr;
+      f.ldc2 = 0;
+      if (type == 1) {  // TRSM(k+1, k): rows 16·part.. of L_ik = A_ik · X_kkᵀ, column blocks w, 7 − w
+        const int64_t r0 = R + 16 * part;
+        f.A = p.A + r0 * lda + K; f.lda = lda;
+        f.B = p.Linv + K * ldl + K; f.ldb = ldl;
+        f.C = p.A + r0 * lda + K; f.ldc = lda;
+        if (p.Lout) { f.C2 = p.Lout + r0 * p.ldlo + K; f.ldc2 = p.ldlo; }
+        f.alpha = 1.0; f.beta = 0.0;
+        f.c0 = wave; f.c1 = 7 - wave; f.ke0 = 16 * (wave + 1); f.ke1 = 16 * (8 - wave);
+        inc = U / NPF_TRSM;
+        out = acnt + ti * T + tk;
+      } else {  // UPD(k+1, k+1, k): row block part >> 1, column block 4·(part & 1) + w (lower only)
+        const int64_t J = 128 * (int64_t)tj, rb = part >> 1, cb = 4 * (part & 1) + wave;
+        f.A = p.A + (R + 16 * rb) * lda + K; f.lda = lda;
+        f.B = p.A + J * lda + K; f.ldb = lda;
+        f.C = p.A + (R + 16 * rb) * lda + J; f.ldc = lda;
+        f.alpha = -1.0; f.beta = 1.0;
+        f.c0 = (ti == tj && cb > rb) ? -1 : (int)cb; f.c1 = -1; f.ke0 = 128; f.ke1 = 0;
+        inc = U / NPF_UPD;
+        out = acnt + ti * T + tj;
+      }
+      run_fine(f);
     } else {
+      inc = U / NP;
       Strip st;
       st.C2 = nullptr;
       st.ldc2 = 0;
@@ -811,9 +932,13 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
 //            the block, leaf 38, strip 9, hand-off 1: the durations the r3 trace measured), so the
 //            updates that feed the next leaves overtake the bulk of the trailing update (the first
 //            leaves waited 20-26 µs behind it).
-// Word: type | part << 3 | i << 8 | j << 16 | k << 24.
-std::vector<uint32_t> dag_task_list(int T, int order) {
+// fine: the leaf chain's TRSM(k+1,k) and UPD(k+1,k+1,k) as fine parts (8 / 16, see run_fine).
+// Word: type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24.
+std::vector<uint32_t> dag_task_list(int T, int order, bool fine) {
   struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0, rank = 0.0; };
+  auto is_fine = [&](const Task& t) {
+    return fine && ((t.type == 1 && t.i == t.k + 1) || (t.type == 2 && t.i == t.k + 1 && t.j == t.i));
+  };
   std::vector<Task> tk;
   std::vector<int> leaf(T), trsm(T * T, -1), fin(T * T, -1);
   std::vector<int> upd_last(T * T, -1), updx_last(T * T, -1);
@@ -852,7 +977,7 @@ std::vector<uint32_t> dag_task_list(int T, int order) {
     for (int t = 0; t < n; ++t)  // generation order is topological
       for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
   } else {
-    auto dur = [&](const Task& t) { return t.type == 0 ? 38.0 : 9.0; };
+    auto dur = [&](const Task& t) { return t.type == 0 ? 38.0 : is_fine(t) ? 4.0 : 9.0; };
     for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
       double m = 0.0;
       for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + 1.0);
@@ -869,10 +994,11 @@ std::vector<uint32_t> dag_task_list(int T, int order) {
     const int t = ready.top().second;
     ready.pop();
     const Task& x = tk[t];
-    const int parts = x.type == 0 ? 1 : dag::NP;
+    const bool f = is_fine(x);
+    const int parts = x.type == 0 ? 1 : !f ? dag::NP : x.type == 1 ? dag::NPF_TRSM : dag::NPF_UPD;
     for (int q = 0; q < parts; ++q)
-      out.push_back((uint32_t)x.type | (uint32_t)q << 3 | (uint32_t)x.i << 8 | (uint32_t)x.j << 16 |
-                    (uint32_t)x.k << 24);
+      out.push_back((uint32_t)x.type | (uint32_t)q << 3 | (uint32_t)f << 7 | (uint32_t)x.i << 8 |
+                    (uint32_t)x.j << 16 | (uint32_t)x.k << 24);
     for (int s2 : succ[t])
       if (!--indeg[s2]) ready.push({tk[s2].est, s2});
   }

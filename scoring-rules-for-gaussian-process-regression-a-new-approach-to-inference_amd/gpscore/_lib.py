@@ -25,6 +25,8 @@ GPS_OPT_DAG_TILES = 13
 GPS_OPT_DAG_GROUP = 17
 GPS_OPT_STREAM_K = 18
 GPS_OPT_DAG_WGS = 19
+GPS_OPT_GEMM_GLDS = 21
+GPS_OPT_DAG_FINE = 22
 GPS_OPT_FORK_MAX = 14
 GPS_OPT_AR_CHUNKS = 15
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
@@ -47,7 +49,7 @@ SIGNATURES = {
     "gps_ctx_synchronize": (_c_int, [_c_vp]),
     "gps_ctx_set_option": (_c_int, [_c_vp, _c_int, _c_int]),
     "gps_ctx_stats": (_c_int, [_c_vp, _c_vp]),
-    "gps_dag_task_list": (_c_int, [_c_int, _c_vp, _c_int]),
+    "gps_dag_task_list": (_c_int, [_c_int, _c_int, _c_vp, _c_int]),
     "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
     "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
     "gps_gram": (_c_int, [_c_vp, _c_int, _P, _c_i64, _P, _c_i64, _c_int, _c_dbl, _P, _c_int,

@@ -13,33 +13,37 @@ import numpy as np
 import pytest
 
 NP_ = 4  # strips per tile task (dag::NP)
+NPF = {1: 8, 2: 16}  # fine parts of the chain's TRSM / UPD (dag::NPF_TRSM, NPF_UPD)
+U = 16   # arrivals per finished tile task (dag::U)
 B = 8    # emulated tile edge (the device uses 128; the algebra is edge-independent)
 
 
-def task_list(T):
+def task_list(T, fine=1):
+    """Queue words decoded as (type, part, i, j, k, fine)."""
     import ctypes
     from gpscore import _lib
     lib = _lib.load()
-    n = lib.gps_dag_task_list(T, None, 0)
+    n = lib.gps_dag_task_list(T, fine, None, 0)
     assert n > 0
     out = (ctypes.c_uint32 * n)()
-    assert lib.gps_dag_task_list(T, ctypes.cast(out, ctypes.c_void_p), n) == n
-    return [(w & 7, (w >> 3) & 3, (w >> 8) & 255, (w >> 16) & 255, (w >> 24) & 255) for w in out]
+    assert lib.gps_dag_task_list(T, fine, ctypes.cast(out, ctypes.c_void_p), n) == n
+    return [(w & 7, (w >> 3) & 15, (w >> 8) & 255, (w >> 16) & 255, (w >> 24) & 255, (w >> 7) & 1)
+            for w in out]
 
 
 def needs(t, T):
     """(counter array, i, j, threshold) pairs a strip task polls (the kernel's switch)."""
-    typ, _, i, j, k = t
+    typ, _, i, j, k, _ = t
     if typ == 0:
-        return [("a", i, i, NP_ * i)]
+        return [("a", i, i, U * i)]
     if typ == 1:
-        return [("a", i, k, NP_ * k), ("a", k, k, NP_ * k + 1)]
+        return [("a", i, k, U * k), ("a", k, k, U * k + 1)]
     if typ == 2:
-        return [("a", i, k, NP_ * (k + 1)), ("a", j, k, NP_ * (k + 1)), ("a", i, j, NP_ * k)]
+        return [("a", i, k, U * (k + 1)), ("a", j, k, U * (k + 1)), ("a", i, j, U * k)]
     if typ == 3:
-        return [("a", i, j, NP_ * (j + 1)), ("x", j, k, 1 if j == k else NP_ * (j - k + 1)),
-                ("x", i, k, NP_ * (j - k))]
-    return [("x", i, k, NP_ * (i - k)), ("x", i, i, 1)]
+        return [("a", i, j, U * (j + 1)), ("x", j, k, 1 if j == k else U * (j - k + 1)),
+                ("x", i, k, U * (j - k))]
+    return [("x", i, k, U * (i - k)), ("x", i, i, 1)]
 
 
 class Emu:
@@ -58,7 +62,9 @@ class Emu:
         return M[i * B:(i + 1) * B, j * B:(j + 1) * B]
 
     def run(self, t):
-        typ, part, i, j, k = t
+        typ, part, i, j, k, fine = t
+        if fine:
+            return self.run_fine(typ, part, i, j, k)
         s = B // NP_  # strip width (32 of 128 on the device)
         rows = slice(part * s, (part + 1) * s)
         if typ == 0:  # LEAF(k = i): the leaf reads A_kk's lower triangle
@@ -70,23 +76,44 @@ class Emu:
         if typ == 1:  # TRSM(i, k): row strip of L_ik = A_ik X_kkᵀ (in place)
             C = self.blk(self.A, i, k)
             C[rows] = C[rows] @ self.blk(self.X, k, k).T
-            self.cnt["a"][i, k] += 1
+            self.cnt["a"][i, k] += U // NP_
         elif typ == 2:  # UPD(i, j, k): row strip of A_ij −= L_ik L_jkᵀ (diagonal: lower blocks)
             C = self.blk(self.A, i, j)
             upd = self.blk(self.A, i, k)[rows] @ self.blk(self.A, j, k).T
             if i == j:  # waves right of the strip's diagonal block stay idle
                 upd[:, (part + 1) * s:] = 0.0
             C[rows] -= upd
-            self.cnt["a"][i, j] += 1
+            self.cnt["a"][i, j] += U // NP_
         elif typ == 3:  # UPDX(i, k, j): row strip of S_ik (+)= L_ij X_jk (first term overwrites)
             C = self.blk(self.X, i, k)
             prod = self.blk(self.A, i, j)[rows] @ self.blk(self.X, j, k)
             C[rows] = prod if j == k else C[rows] + prod
-            self.cnt["x"][i, k] += 1
+            self.cnt["x"][i, k] += U // NP_
         else:  # FIN(i, k): column strip of X_ik = −X_ii S_ik (in place)
             C = self.blk(self.X, i, k)
             C[:, rows] = -self.blk(self.X, i, i) @ C[:, rows]
-            self.cnt["x"][i, k] += 1
+            self.cnt["x"][i, k] += U // NP_
+
+    def run_fine(self, typ, part, i, j, k):
+        """The chain's fine parts: TRSM(k+1,k) by 16-row strips (B/8 here), UPD(k+1,k+1,k) by
+        (row block, column half) with the blocks right of the diagonal block idle."""
+        e = B // 8  # the device's 16-row block
+        if typ == 1:
+            assert i == k + 1
+            C = self.blk(self.A, i, k)
+            rows = slice(part * e, (part + 1) * e)
+            C[rows] = C[rows] @ self.blk(self.X, k, k).T
+            self.cnt["a"][i, k] += U // NPF[1]
+            return
+        assert typ == 2 and i == j == k + 1
+        rb, h = part >> 1, part & 1
+        rows, cols = slice(rb * e, (rb + 1) * e), slice(h * B // 2, (h + 1) * B // 2)
+        upd = self.blk(self.A, i, k)[rows] @ self.blk(self.A, j, k)[cols].T
+        for c in range(upd.shape[1]):  # column block of the wave
+            if (h * B // 2 + c) // e > rb:
+                upd[:, c] = 0.0
+        self.blk(self.A, i, j)[rows, cols] -= upd
+        self.cnt["a"][i, j] += U // NPF[2]
 
 
 def spd(T, seed):
@@ -107,9 +134,10 @@ def check(em, A):
     assert np.allclose(X, np.linalg.inv(Lr), rtol=1e-11, atol=1e-11)
 
 
+@pytest.mark.parametrize("fine", [0, 1])
 @pytest.mark.parametrize("T", [2, 3, 5, 8, 13])
-def test_queue_order_is_topological(T):
-    tl = task_list(T)
+def test_queue_order_is_topological(T, fine):
+    tl = task_list(T, fine)
     A = spd(T, T)
     em = Emu(A, T)
     for t in tl:
@@ -118,13 +146,20 @@ def test_queue_order_is_topological(T):
     check(em, A)
     kinds = [t[0] for t in tl]
     assert kinds.count(0) == T
-    assert kinds.count(1) == NP_ * T * (T - 1) // 2 and kinds.count(4) == NP_ * T * (T - 1) // 2
+    nf = sum(t[5] for t in tl if t[0] == 1)
+    assert nf == (NPF[1] * (T - 1) if fine else 0)
+    assert kinds.count(1) == NP_ * T * (T - 1) // 2 + nf * (1 - NP_ / NPF[1])
+    assert kinds.count(4) == NP_ * T * (T - 1) // 2
+    assert all(t[1] < (NPF[t[0]] if t[5] else NP_ if t[0] else 1) for t in tl)
+    # the fine parts are exactly the chain's TRSM(k+1,k) and UPD(k+1,k+1,k)
+    assert all(t[2] == t[4] + 1 and (t[0] == 1 or t[3] == t[2]) for t in tl if t[5])
 
 
+@pytest.mark.parametrize("fine", [0, 1])
 @pytest.mark.parametrize("T,seed", [(4, 0), (6, 1), (9, 2)])
-def test_counters_cover_every_dependency(T, seed):
+def test_counters_cover_every_dependency(T, seed, fine):
     """Random execution orders permitted by the thresholds alone (any worker timing)."""
-    tl = task_list(T)
+    tl = task_list(T, fine)
     A = spd(T, 10 + seed)
     em = Emu(A, T)
     rng = np.random.default_rng(seed)
@@ -141,11 +176,12 @@ def test_queue_sizes():
     from gpscore import _lib
     lib = _lib.load()
     for T in (2, 20, 40):
-        n = lib.gps_dag_task_list(T, None, 0)
         upd = T * (T - 1) * (T + 1) // 6          # Σ_k (T−1−k)(T−k)/2
         updx = (T - 1) * T * (T + 1) // 6         # Σ_j (T−1−j)(j+1)
-        assert n == T + NP_ * (T * (T - 1) + upd + updx)
-    assert lib.gps_dag_task_list(65, None, 0) < 0 and lib.gps_dag_task_list(1, None, 0) < 0
+        n0 = T + NP_ * (T * (T - 1) + upd + updx)
+        assert lib.gps_dag_task_list(T, 0, None, 0) == n0
+        assert lib.gps_dag_task_list(T, 1, None, 0) == n0 + (T - 1) * (NPF[1] + NPF[2] - 2 * NP_)
+    assert lib.gps_dag_task_list(65, 1, None, 0) < 0 and lib.gps_dag_task_list(1, 1, None, 0) < 0
 
 
 def test_dag_kernel_loop_is_uniform():

@@ -2,7 +2,7 @@
 // of T 128-tiles, standalone: timing over repeated launches, a sampled correctness check
 // (L·Lᵀ = A and L⁻¹·L = I on random entries), and one traced launch whose per-slot timestamps
 // go to a CSV for tools/dag_trace.py (critical path, hand-off latencies, per-type durations).
-//   dag_bench [T=20] [nwg=256] [trace.csv|-] [reps=20] [group=3] [order=1]
+//   dag_bench [T=20] [nwg=256] [trace.csv|-] [reps=20] [group=3] [order=1] [fine=1]
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -24,6 +24,7 @@ int main(int argc, char** argv) {
   const int reps = argc > 4 ? atoi(argv[4]) : 20;
   const int group = argc > 5 ? atoi(argv[5]) : 3;
   const int order = argc > 6 ? atoi(argv[6]) : 1;
+  const int fine = argc > 7 ? atoi(argv[7]) : 1;
   const int n = 128 * T, d = 8;
   // SPD test block: ARD-style Gram of random points + noise (what the recursion hands down)
   std::mt19937_64 rng(7);
@@ -36,7 +37,7 @@ int main(int argc, char** argv) {
       for (int k = 0; k < d; ++k) { const double t = X[i * d + k] - X[j * d + k]; s += t * t; }
       h[(size_t)i * n + j] = exp(-0.25 * s) + (i == j ? 0.05 : 0.0);
     }
-  const std::vector<uint32_t> tl = dag_task_list(T, order);
+  const std::vector<uint32_t> tl = dag_task_list(T, order, fine != 0);
   const int nt = (int)tl.size();
   double *A0, *A, *Li, *ld;
   int *info, *cnt;
@@ -107,7 +108,7 @@ int main(int argc, char** argv) {
   double lsum = 0;
   for (double x : gld) lsum += x;
   const double fl = 2.0 * n * (double)n * n / 3.0;
-  printf("group=%d order=%d ", group, order);
+  printf("group=%d order=%d fine=%d ", group, order, fine);
   printf("T=%d n=%d nwg=%d tasks=%d: median %.3f ms (min %.3f, max %.3f) = %.1f us/tile, %.2f TF/s; "
          "max|XAX^T - I| %.2e over 24 samples, sum log L_ii %.6f\n",
          T, n, nwg, nt, ts[ts.size() / 2], ts[0], ts.back(), 1e3 * ts[ts.size() / 2] / T,

@@ -15,7 +15,7 @@ def load(path):
     rows = []
     for r in csv.DictReader(open(path)):
         w = int(r["word"])
-        rows.append(dict(slot=int(r["slot"]), type=w & 7, part=(w >> 3) & 3, i=(w >> 8) & 255,
+        rows.append(dict(slot=int(r["slot"]), type=w & 7, part=(w >> 3) & 15, fine=(w >> 7) & 1, i=(w >> 8) & 255,
                          j=(w >> 16) & 255, k=(w >> 24) & 255, fetch=int(r["fetch"]),
                          ready=int(r["ready"]), done=int(r["done"]), wg=int(r["wg"]),
                          xcc=int(r["xcc"])))
