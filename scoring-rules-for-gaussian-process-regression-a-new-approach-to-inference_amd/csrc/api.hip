@@ -584,8 +584,10 @@ size_t potrf_ws_doubles(int64_t n_pad) {
   return (size_t)std::max<int64_t>(tot, GPS_TILE * GPS_TILE);
 }
 
-// factor the padded SPD matrix in A (destroyed) into Linv (must be zero in strict-upper
-// tiles), logdiag (n_pad).  Returns 0 or the LAPACK-style info (> 0).
+// factor the padded SPD matrix in A (destroyed) into Linv, logdiag (n_pad).  Linv (and Lout)
+// must hold zeros above the diagonal already — every caller memsets the buffer when it allocates
+// or resizes it; the factorisation writes the lower triangle only, the diagonal 16×16 tiles of
+// the leaves included.  Returns 0 or the LAPACK-style info (> 0).
 int reset_info(gps_ctx* ctx) {  // [first non-PD minor, persistent-kernel error]
   HIPCHK(hipMemsetAsync(ctx->info.p, 0x7f, 2 * sizeof(int), ctx->stream));
   return 0;

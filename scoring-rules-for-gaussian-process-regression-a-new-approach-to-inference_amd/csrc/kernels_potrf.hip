@@ -205,6 +205,62 @@ __device__ __forceinline__ constexpr int tile_i(int t) {
   return t < 1 ? 0 : t < 3 ? 1 : t < 6 ? 2 : t < 10 ? 3 : t < 15 ? 4 : t < 21 ? 5 : t < 28 ? 6 : 7;
 }
 
+// Phase A's trailing tiles per (step p, rank of the update wave): every 5th tile to the wave that
+// also inverts L_{p-1,p-1}, the rest alternating over the other two; a table (dwords: dst | a << 8
+// | b << 16, scalar loads) so that a wave can batch its tiles.  With one wave per SIMD a dependent
+// f64 MFMA costs ~200 cycles and an independent one ~140 (tools/mfma_f64_probe.hip, r4): a tile's
+// 4-MFMA chain alone, after its LDS reads, took ~1k cycles; three tiles per group interleave their
+// chains (phase A of the first steps 10.3k -> 7.6k cycles, tools/leaf_probe.hip).
+struct Deal {
+  int n[8][3];
+  unsigned int t[8][3][12];
+};
+constexpr Deal make_deal() {
+  Deal d{};
+  for (int p = 1; p < 8; ++p) {
+    int task = 0;
+    for (int j = p + 1; j < 8; ++j)
+      for (int i = j; i < 8; ++i, ++task) {
+        const int who = task % 5 == 4 ? 0 : 1 + ((task - task / 5) & 1);
+        d.t[p][who][d.n[p][who]++] =
+            (unsigned)tix(i, j) | (unsigned)tix(i, p - 1) << 8 | (unsigned)tix(j, p - 1) << 16;
+      }
+  }
+  return d;
+}
+__constant__ Deal g_deal = make_deal();
+
+// S_dst[u] −= L_a[u] L_b[u]ᵀ for up to G tiles of the list: every LDS read of the group, then the
+// MFMAs (G independent chains, each tile's in tile_update's order: the same bits), then the writes
+template <int G>
+__device__ __forceinline__ void tile_update_group(double* S, const unsigned int* tl, int cnt, int lane) {
+  d4 c[G];
+  double a[G][4], b[G][4];
+  int td[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    if (u < cnt) {
+      const unsigned w = tl[u];
+      td[u] = w & 255;
+      const int ta = (w >> 8) & 255, tb = w >> 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[u][q] = S[acc_off(td[u], lane, q)];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) { a[u][kk] = -opnd(S, ta, lane, kk); b[u][kk] = opnd(S, tb, lane, kk); }
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      if (u < cnt) c[u] = mfma(a[u][kk], b[u][kk], c[u]);
+#pragma unroll
+  for (int u = 0; u < G; ++u)
+    if (u < cnt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S[acc_off(td[u], lane, q)] = c[u][q];
+}
+
 // T_k = Σ_{j=k}^{r-1} L_{r,j} X_{j,k} (two accumulators: the MFMA chain is half as long)
 __device__ __forceinline__ d4 inv_row_t(const double* S, int r, int k, int lane) {
   d4 e0 = (d4){0.0, 0.0, 0.0, 0.0}, e1 = e0;
@@ -243,7 +299,9 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
                                           double* __restrict__ Lout, int64_t ldlo,
                                           double* __restrict__ logdiag, int* info, int base,
                                           int nreal, double* S, double* DG) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // the wave index as a scalar: its branches and the tile-table loads then stay on the scalar unit
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // ---- A's lower tiles into LDS (all 18 loads of a thread in flight at once); zeros into
   //      Linv above the tile diagonal
   {
@@ -290,11 +348,10 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
 #pragma unroll
           for (int c = 0; c < 16; ++c) S[t + c] = P[s][c];
         }
-        if (Lout) {
+        if (Lout && R >= t0) {
           dv2* dst = reinterpret_cast<dv2*>(Lout + (int64_t)R * ldlo + t0);
 #pragma unroll
-          for (int c = 0; c < 8; ++c)
-            dst[c] = R >= t0 ? (dv2){P[s][2 * c], P[s][2 * c + 1]} : (dv2){0.0, 0.0};
+          for (int c = 0; c < 8; ++c) dst[c] = (dv2){P[s][2 * c], P[s][2 * c + 1]};
         }
       }
     } else if (p >= 1) {
@@ -303,13 +360,8 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
       // other two first, the T_k tasks to all three
       const int winv = pp % 3;
       const int rank = (uw - winv + 3) % 3;  // 0: the inverting wave
-      int task = 0;
-      for (int j = p + 1; j < 8; ++j)
-        for (int i = j; i < 8; ++i, ++task) {
-          // deal order: rank 1, rank 2, rank 1, rank 2, ... with every 5th tile to rank 0
-          const int who = task % 5 == 4 ? 0 : 1 + ((task - task / 5) & 1);
-          if (who == rank) tile_update(S, tix(i, j), tix(i, pp), tix(j, pp), lane);
-        }
+      const int nt = g_deal.n[p][rank];
+      for (int g0 = 0; g0 < nt; g0 += 3) tile_update_group<3>(S, g_deal.t[p][rank] + g0, nt - g0, lane);
       if (rank == 0) {
         invert_diag<COH>(S, DG, pp, lane, Linv, ldl);
         if (lane < 16) logdiag[16 * pp + lane] = log(DG[16 * pp + lane]);
@@ -382,17 +434,10 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
   } else if (tid >= 240) {
     logdiag[112 + tid - 240] = log(DG[112 + tid - 240]);
   }
-  {  // zeros above the tile diagonal of Linv: the 28 upper tiles, 14 dv2 per thread
-    const int hb = tid >> 7, q = tid & 127, r = q >> 3, c2 = (q & 7) * 2;
-#pragma unroll
-    for (int m = 0; m < 14; ++m) {
-      const int u = 2 * m + hb;  // upper tile u: (i, j), i < j, row-major over i
-      const int ui = u < 7 ? 0 : u < 13 ? 1 : u < 18 ? 2 : u < 22 ? 3 : u < 25 ? 4 : u < 27 ? 5 : 6;
-      const int ustart = ui * 7 - ui * (ui - 1) / 2;  // first upper tile of row ui
-      const int uj = ui + 1 + (u - ustart);
-      st_d2<COH>(Linv + (int64_t)(16 * ui + r) * ldl + 16 * uj + c2, (dv2){0.0, 0.0});
-    }
-  }
+  // (the 28 16×16 tiles above the tile diagonal of Linv, and Lout's rows above each column
+  // panel, are not written: every caller zeroes the factor buffers when it (re)allocates them and
+  // nothing writes there afterwards — round 4: 57 KB less write-through traffic to drain at the
+  // end of every persistent LEAF)
 }
 
 __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
