@@ -712,8 +712,13 @@ __device__ __forceinline__ void run_fine(const Fine& s) {
 // zero at launch, zero again when the last workgroup leaves.
 // TRACE: per queue slot t, trace[4t..4t+3] = {fetched, inputs ready, outputs drained} in 100 MHz
 // s_memrealtime ticks and (blockIdx << 8 | XCC id) — the diagnostics launch (tools/dag_bench.cpp)
+// (GPS_DAG_WAVES_PER_EU: a build knob for tools/dag_bench.cpp A/B runs — 2 asks the compiler for
+// two workgroups per CU, i.e. ≤ 256 registers per lane, at the cost of scratch spills)
+#ifndef GPS_DAG_WAVES_PER_EU
+#define GPS_DAG_WAVES_PER_EU 1
+#endif
 template <bool TRACE, int G>
-__global__ __launch_bounds__(256) void potrf_dag_kernel(DagParams p) {
+__global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(DagParams p) {
   __shared__ double S[v4::NT * v4::TSZ];
   __shared__ double DG[128];
   __shared__ unsigned int sh[3];  // [task word, abort, queue slot]
