@@ -35,15 +35,22 @@ void run(int threads, int blocks, int iters) {
   hipMalloc(&out, (size_t)blocks * threads * 8); hipMalloc(&clk, 16);
   rate<NACC><<<blocks, threads>>>(out, clk, iters, 1e-3);
   hipDeviceSynchronize();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipEventRecord(e0);
   rate<NACC><<<blocks, threads>>>(out, clk, iters, 1e-3);
-  hipDeviceSynchronize();
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double tflops = (double)blocks * (threads / 64) * iters * NACC * 2048.0 / (ms * 1e-3) / 1e12;
   unsigned long long h[2];
   hipMemcpy(h, clk, 16, hipMemcpyDeviceToHost);
   const double cyc = (double)h[0], us = h[1] / 100.0;
   const int waves_per_simd = (threads / 64 + 3) / 4;  // one block per CU (blocks = CUs)
   printf("NACC=%2d waves/SIMD=%d: %.1f shader cycles per MFMA per wave, SIMD issue every %.1f cycles "
-         "(clock %.2f GHz)\n", NACC, waves_per_simd, cyc / ((double)iters * NACC),
-         cyc / ((double)iters * NACC * waves_per_simd), cyc / us / 1e3);
+         "(clock %.2f GHz); chip %.1f TF/s over %.3f ms\n", NACC, waves_per_simd, cyc / ((double)iters * NACC),
+         cyc / ((double)iters * NACC * waves_per_simd), cyc / us / 1e3, tflops, ms);
   hipFree(out); hipFree(clk);
 }
 
