@@ -207,10 +207,11 @@ __device__ __forceinline__ constexpr int tile_i(int t) {
 
 // Phase A's trailing tiles per (step p, rank of the update wave): every 5th tile to the wave that
 // also inverts L_{p-1,p-1}, the rest alternating over the other two; a table (dwords: dst | a << 8
-// | b << 16, scalar loads) so that a wave can batch its tiles.  With one wave per SIMD a dependent
-// f64 MFMA costs ~200 cycles and an independent one ~140 (tools/mfma_f64_probe.hip, r4): a tile's
-// 4-MFMA chain alone, after its LDS reads, took ~1k cycles; three tiles per group interleave their
-// chains (phase A of the first steps 10.3k -> 7.6k cycles, tools/leaf_probe.hip).
+// | b << 16, scalar loads) so that a wave can batch its tiles.  A tile update cost ~1k cycles
+// one at a time (its LDS reads, then a 4-MFMA chain of 64 cycles each — one wave per SIMD issues
+// f64 MFMAs at the full rate, dependent or not: tools/mfma_f64_rate.hip — then the result wait
+// before the writes); three tiles per group overlap those latencies (phase A of the first steps
+// 10.3k -> 7.6k cycles, tools/leaf_probe.hip).
 struct Deal {
   int n[8][3];
   unsigned int t[8][3][12];

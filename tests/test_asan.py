@@ -11,6 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd")
 ASAN_LIB = os.path.join(PKG, "gpscore", "libgpscore_asan.so")
 ASAN_RT = "/opt/rocm/lib/llvm/lib/clang/22/lib/linux/libclang_rt.asan-x86_64.so"
+HSA_RT = "/opt/rocm/lib/libhsa-runtime64.so.1"
 
 
 def _run(mode):
@@ -21,8 +22,16 @@ def _run(mode):
         rt = subprocess.run(["/opt/rocm/bin/hipcc", "-print-file-name=libclang_rt.asan-x86_64.so"],
                             capture_output=True, text=True).stdout.strip()
     env = dict(os.environ)
-    env["LD_PRELOAD"] = rt + ((" " + env["LD_PRELOAD"]) if env.get("LD_PRELOAD") else "")
-    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1:halt_on_error=1"
+    # The HSA runtime goes ahead of the ASan runtime: the ASan runtime's own interceptor of
+    # hsa_amd_memory_pool_allocate (its GPU-ASan support, which needs XNACK-enabled device code)
+    # ran out of memory at HIP's first device allocation on every pool box (r4:
+    # gpurun_out/asan_dev_a1.err); preloaded first, libhsa-runtime64 keeps its own definition of the
+    # hsa_* symbols for HIP, while malloc / free and the other host interceptors stay ASan's (the
+    # first preloaded library that defines them).  That order needs verify_asan_link_order=0.
+    pre = [HSA_RT] if os.path.exists(HSA_RT) else []
+    env["LD_PRELOAD"] = " ".join(pre + [rt] + ([env["LD_PRELOAD"]] if env.get("LD_PRELOAD") else []))
+    env["ASAN_OPTIONS"] = ("detect_leaks=0:abort_on_error=1:halt_on_error=1"
+                           + (":verify_asan_link_order=0" if pre else ""))
     env["GPSCORE_LIB"] = ASAN_LIB
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asan_check.py"), mode],
                        env=env, capture_output=True, text=True, timeout=240)

@@ -79,7 +79,7 @@ def device_mode(lib):
         ("gps_fitc_set_data", (h, P(X), P(y), 0, 3, 0.0, 1.0, 0)),
         ("gps_fitc_fit", (h, P(th), 1, P(obj), None, None)),
         ("gps_ctx_set_option", (h, 99, 1)),
-        ("gps_full_surface", (h, P(X), P(y), 300, 3, 0.0, P(th), 1, P(th), 1, 0, P(np.zeros(4)))),
+        ("gps_full_surface", (h, P(X), P(y), 300, 3, 0.0, P(th), 0, P(th), 1, 0, P(np.zeros(4)))),
         ("gps_full_surface", (h, P(X), P(y), 10, 3, 0.0, P(th), 1, P(th), 1, 8, P(np.zeros(4)))),
         ("gps_comm_init", (h, 0, 0, None)),
         ("gps_comm_init_local", (h, 2, 5, 1)),
