@@ -115,6 +115,10 @@ enum {
                              diagonal update as fine parts (16×16 blocks per wave, 8 / 16 workgroups
                              per tile); 0: as 4 row strips like every other tile task.  Same values
                              (the strips add exact zero products above X_kk's diagonal). */
+  GPS_OPT_DAG_SPLIT = 23, /* 1: the persistent factorisation's chain without the leaf's inverse —
+                             LEAF' factors and inverts only the 16×16 diagonal blocks, TRSM(k+1,k)
+                             substitutes with them, an INV task forms L_kk⁻¹ off the chain;
+                             0 (default): the leaf forms L_kk and L_kk⁻¹ together. */
   GPS_OPT_GEMM_GLDS = 21, /* 1: 128-tile GEMM launches stage their operands global -> LDS directly
                              (global_load_lds) instead of through registers; 0 (default).  Same
                              values bitwise.  Process-wide. */
@@ -136,9 +140,10 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
 
 /* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one
  * word per strip task (type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24; types 0 LEAF,
- * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN; fine: the chain tasks' parts as GPS_OPT_DAG_FINE —
- * kernels_potrf.hip).  Returns the queue length (writes at most cap words); needs no device. */
-int gps_dag_task_list(int T, int fine, uint32_t* out, int cap);
+ * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN, 5 LEAF', 6 INV, 7 TRSM'; flags bit 0: the chain tasks' fine
+ * parts (GPS_OPT_DAG_FINE), bit 1: the split chain (GPS_OPT_DAG_SPLIT) — kernels_potrf.hip).
+ * Returns the queue length (writes at most cap words); needs no device. */
+int gps_dag_task_list(int T, int flags, uint32_t* out, int cap);
 
 /* on: 0 off, 1 per-kernel-class tags, 2 GEMM tags also carry layout/shape/tri/split-K/lda */
 int gps_prof_enable(gps_ctx* ctx, int on);

@@ -106,8 +106,9 @@ struct gps_ctx {
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
   int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: automatic, see dag_width)
   bool dag_fine = true;                // GPS_OPT_DAG_FINE
+  bool dag_split = false;              // GPS_OPT_DAG_SPLIT
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
-  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2T + fine: device task list, length
+  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 4T + 2 split + fine: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
   int64_t dag_cnt_used = 0;
@@ -442,6 +443,11 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
   return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
 
+// the task list of an nb-tile persistent block under the context's options
+int dag_list_key(const gps_ctx* ctx, int64_t nb) {
+  return (int)(4 * nb + 2 * (ctx->dag_split ? 1 : 0) + (ctx->dag_fine ? 1 : 0));
+}
+
 // a block of nb 128-tiles goes to the persistent factorisation (GPS_OPT_DAG)
 bool dag_block(const gps_ctx* ctx, int64_t nb) { return ctx->dag && nb >= 2 && nb <= ctx->dag_tiles; }
 
@@ -478,7 +484,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     return 0;
   }
   if (dag_block(ctx, nb)) {  // the whole block in one persistent launch (kernels_potrf.hip)
-    auto it = ctx->dag_lists.find(2 * nb + ctx->dag_fine);
+    auto it = ctx->dag_lists.find(dag_list_key(ctx, nb));
     const int64_t need = dag_cnt_ints(nb);
     if (it == ctx->dag_lists.end() || ctx->dag_cnt_used + need > (int64_t)(ctx->dag_cnt.cap / 4))
       return fail(ctx, -2, "persistent factorisation: task list / counters not prepared");
@@ -489,6 +495,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     d.cnt = static_cast<int*>(ctx->dag_cnt.p) + ctx->dag_cnt_used;
     d.spin_ticks = 200000000ull;  // 2 s at the 100 MHz real-time clock
     d.group = ctx->dag_group;
+    d.split = ctx->dag_split ? 1 : 0;
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
@@ -613,9 +620,9 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   int64_t dcnt = 0;
   dag_blocks(ctx, n_pad / GPS_TILE, dsizes, dcnt);
   for (int T : dsizes) {
-    const int lk = 2 * T + ctx->dag_fine;
+    const int lk = dag_list_key(ctx, T);
     if (ctx->dag_lists.count(lk)) continue;
-    const std::vector<uint32_t> tl = dag_task_list(T, 1, ctx->dag_fine);
+    const std::vector<uint32_t> tl = dag_task_list(T, 1, ctx->dag_fine, ctx->dag_split);
     auto& e = ctx->dag_lists[lk];
     HIPCHK(ensure(ctx, e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
@@ -655,7 +662,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
       (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_half,
       (uintptr_t)ctx->dag_cnt.p, (uintptr_t)ctx->sk_cnt.p};
-  for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[2 * T + ctx->dag_fine].first.p);  // the task lists
+  for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[dag_list_key(ctx, T)].first.p);  // the task lists
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
       g.last_use = ++ctx->graph_tick;
@@ -1349,6 +1356,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->dag_wgs = value;
       return 0;
     case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
+    case GPS_OPT_DAG_SPLIT: ctx->dag_split = value != 0; return 0;
     case GPS_OPT_DAG_GROUP:
       ARGCHK(value >= 2 && value <= 4, "GPS_OPT_DAG_GROUP must be 2, 3 or 4");
       ctx->dag_group = value;
@@ -1383,9 +1391,9 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
   return 0;
 }
 
-int gps_dag_task_list(int T, int fine, uint32_t* out, int cap) {
+int gps_dag_task_list(int T, int flags, uint32_t* out, int cap) {
   if (T < 2 || T > 64 || cap < 0 || (cap > 0 && !out)) return fail(nullptr, -1, "bad arguments");
-  const std::vector<uint32_t> tl = dag_task_list(T, 1, fine != 0);
+  const std::vector<uint32_t> tl = dag_task_list(T, 1, (flags & 1) != 0, (flags & 2) != 0);
   for (int i = 0; i < cap && i < (int)tl.size(); ++i) out[i] = tl[i];
   return (int)tl.size();
 }

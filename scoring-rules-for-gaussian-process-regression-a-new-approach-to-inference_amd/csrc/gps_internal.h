@@ -254,9 +254,10 @@ struct DagParams {
   unsigned long long spin_ticks;   // 100 MHz s_memrealtime ticks a dependency wait may take
   unsigned long long* trace = nullptr;  // diagnostics only (tools/dag_bench.cpp): 4 words per slot
   int group = 3;                   // 16-deep operand chunks per load group of a strip task (2..4)
+  int split = 0;                   // the task list is a split-chain one (dag_task_list split)
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
-std::vector<uint32_t> dag_task_list(int T, int order = 1, bool fine = true);
+std::vector<uint32_t> dag_task_list(int T, int order = 1, bool fine = true, bool split = false);
 inline int64_t dag_cnt_ints(int T) { return (16 + 2 * (int64_t)T * T + 63) / 64 * 64; }
 
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)

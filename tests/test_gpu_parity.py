@@ -835,3 +835,44 @@ def test_gemm_glds_bitwise(gpu_ctx):
         gpu_ctx.call("gps_ctx_set_option", 21, 0)
     for a, b in zip(gl, base):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("n,tiles", [(2560, 20), (5000, 20), (4000, 40)])
+def test_persistent_split_chain(gpu_ctx, n, tiles):
+    """GPS_OPT_DAG_SPLIT: the persistent factorisation's chain without the leaf's inverse (LEAF'
+    forms L_kk and the 16×16 diagonal inverses, TRSM'(k+1,k) substitutes with them, INV forms
+    L_kk⁻¹ off the chain) against the default chain — the same factorisation in another rounding
+    order (substitution instead of the product with L_kk⁻¹): LOO, predictive outputs and
+    objectives within 1e-11 relative and against the oracle; a refit and any launch width give
+    the same bits.  Reference: torch.potrf KF:26 / KF:332, chol_solve(I, A) KF:242."""
+    import gpscore
+    from gpscore import _lib
+    rng = np.random.default_rng(n + 7)
+    d = 5
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((300, d))
+    y, yt = np.cos(X.sum(1)) + 0.1 * rng.standard_normal(n), np.cos(Xt.sum(1))
+    th = (0.1, np.log(1.5) * np.ones(d), np.log(0.03))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    runs = []
+    try:
+        gpu_ctx.set_dag(True, tiles)
+        for split, wgs in ((0, 0), (1, 0), (1, 0), (1, 4)):
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_SPLIT, split)
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_WGS, wgs)
+            r = gp.fit(X, y, th)
+            mu, var = gp.predict(Xt, yt)
+            runs.append((r, mu, var))
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_SPLIT, 0)
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_WGS, 0)
+        gpu_ctx.set_dag(True, 20)
+    (r0, mu0, var0), (r1, mu1, var1) = runs[0], runs[1]
+    for r, mu, var in runs[2:]:
+        assert r.objectives == r1.objectives and np.array_equal(mu, mu1) and np.array_equal(var, var1)
+        assert np.array_equal(r.mu_loo, r1.mu_loo) and np.array_equal(r.var_loo, r1.var_loo)
+    for a, b in ((r1.mu_loo, r0.mu_loo), (r1.var_loo, r0.var_loo), (mu1, mu0), (var1, var0)):
+        assert nrel(a, b) < 1e-11
+    for k in ("nlml", "loo_crps", "loo_logs", "logdet", "quad"):
+        assert abs(r1.objectives[k] - r0.objectives[k]) <= 1e-11 * max(1.0, abs(r0.objectives[k])), k
+    f = O.fast_full_fit(X, y, *th)
+    assert nrel(r1.mu_loo, f["loo_mu"]) < 1e-9 and nrel(r1.var_loo, f["loo_var"]) < 1e-9

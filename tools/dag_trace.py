@@ -7,7 +7,7 @@ import csv
 import sys
 from collections import defaultdict
 
-NAMES = {0: "LEAF", 1: "TRSM", 2: "UPD", 3: "UPDX", 4: "FIN"}
+NAMES = {0: "LEAF", 1: "TRSM", 2: "UPD", 3: "UPDX", 4: "FIN", 5: "LEAF'", 6: "INV", 7: "TRSM'"}
 TICK_US = 0.01  # s_memrealtime runs at 100 MHz
 
 
@@ -49,13 +49,14 @@ def main():
     print("\nleaf chain: k, LEAF ready/run, ->TRSM(k+1,k) hand-off + run, ->UPD(k+1,k+1,k) hand-off + run, ->LEAF(k+1) hand-off")
     tot = defaultdict(float)
     for k in range(T):
-        lk = (0, k, k, k)
+        lt = 5 if (5, k, k, k) in done else 0
+        lk = (lt, k, k, k)
         line = f"k={k:2d} leaf @{ready[lk]:8.1f} run {done[lk] - ready[lk]:6.1f}"
         tot["leaf"] += done[lk] - ready[lk]
         if k + 1 < T:
-            tr = (1, k + 1, k, k)
+            tr = (7 if (7, k + 1, k, k) in done else 1, k + 1, k, k)
             up = (2, k + 1, k + 1, k)
-            nl = (0, k + 1, k + 1, k + 1)
+            nl = (lt, k + 1, k + 1, k + 1)
             h1 = ready[tr] - done[lk]
             r1 = done[tr] - ready[tr]
             h2 = ready[up] - done[tr]
@@ -66,7 +67,7 @@ def main():
             tot["upd"] += r2
             line += f" | trsm +{h1:5.1f} run {r1:5.1f} | upd +{h2:5.1f} run {r2:5.1f} | leaf +{h3:5.1f}"
         print(line)
-    last_leaf = done[(0, T - 1, T - 1, T - 1)]
+    last_leaf = done[(5 if (5, T - 1, T - 1, T - 1) in done else 0, T - 1, T - 1, T - 1)]
     print(f"\nchain totals: leaves {tot['leaf']:.1f} us, TRSM runs {tot['trsm']:.1f}, UPD runs {tot['upd']:.1f}, "
           f"hand-offs {tot['h']:.1f}; last leaf done @{last_leaf:.1f}, tail (inverse) {span - last_leaf:.1f} us")
     busy = sum(r["done"] - r["ready"] for r in rows)
