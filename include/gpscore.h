@@ -115,6 +115,12 @@ enum {
                              diagonal update as fine parts (16×16 blocks per wave, 8 / 16 workgroups
                              per tile); 0: as 4 row strips like every other tile task.  Same values
                              (the strips add exact zero products above X_kk's diagonal). */
+  GPS_OPT_GEMM_PRIO = 24, /* raised wave priority (s_setprio 1) around the GEMM mainloop's MFMA
+                             phase, so that the other workgroup's waves on the SIMD issue their
+                             loads and LDS writes behind it: 1 (default) for the product and
+                             column-reduction launches (C3 −1.1 %), 2 for every launch (the FITC
+                             row-norm and Λ-scaled SYRK launches ran 0.4 % slower), 0 off.  Same
+                             values.  Process-wide. */
   GPS_OPT_DAG_SPLIT = 23, /* 1: the persistent factorisation's chain without the leaf's inverse —
                              LEAF' factors and inverts only the 16×16 diagonal blocks, TRSM(k+1,k)
                              substitutes with them, an INV task forms L_kk⁻¹ off the chain;

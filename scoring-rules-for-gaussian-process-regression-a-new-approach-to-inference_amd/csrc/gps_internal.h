@@ -74,6 +74,7 @@ struct GemmParams {
   int sk_slots;              // workgroup slots of the chip (2 per CU for the 128-tile kernel)
   // set by launch_gemm for the stream-K tail: tiles [sk_dp, tiles) are split over sk_wgs blocks
   int sk_dp, sk_wgs;
+  int prio;                  // 1: the mainloop's MFMA phase at raised wave priority (g_gemm_prio)
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
@@ -83,6 +84,7 @@ extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resi
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 extern int g_stream_k;   // 1: the stream-K tail of uniform-K 128-tile launches (launch_gemm)
 extern int g_gemm_glds;  // 1: 128-tile launches stage operands global -> LDS directly (glds)
+extern int g_gemm_prio;  // s_setprio around the mainloop's MFMA phase: 0 off, 1 (default) products, 2 all
 constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)
 
 // ------------------------------------------------------------ device reductions

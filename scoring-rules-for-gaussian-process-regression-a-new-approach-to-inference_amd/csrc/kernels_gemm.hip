@@ -490,7 +490,9 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     // park the prefetched slice in the other LDS buffer (no branches in the body)
     for (int it = 0; it < nk - 1; ++it) {
       load_tile(kb + (it + 1) * BK);
+      if (p.prio) __builtin_amdgcn_s_setprio(1);
       compute(it & 1);
+      if (p.prio) __builtin_amdgcn_s_setprio(0);
       row_dot(it & 1, kb + it * BK);
       store_tile((it + 1) & 1);
       __syncthreads();
@@ -753,7 +755,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
 }
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
-int g_gemm_glds = 0;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
+int g_gemm_glds = 0;
+int g_gemm_prio = 1;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
 int g_stream_k = 0;   // GPS_OPT_STREAM_K (process-wide; off: DESIGN §6.20)
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
@@ -888,6 +891,9 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
       tiles = q.sk_dp + slots;
     }
   }
+  // raised MFMA-phase priority: 1 = the product / column-reduction launches only (C3 −1.3 %;
+  // the FITC row-norm launches and the Λ-scaled SYRK ran 0.4 % slower with it), 2 = every launch
+  q.prio = g_gemm_prio == 2 || (g_gemm_prio == 1 && (epi == EPI_STORE || epi == EPI_COLRED) && !q.kscale);
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
   // direct-to-LDS staging (GPS_OPT_GEMM_GLDS): 128-tiles without a per-k operand scale, the
