@@ -159,6 +159,7 @@ struct gps_ctx {
   // FITC gradient: the fold's G_f, E_f, G_fE_f and F = Gblk E; energy score: work area, draws
   DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
   DBuf ebuf_aux[3], bPIs, bRW;  // concurrent ES folds: work areas of the aux streams, C_f, r_f / w_f
+  DBuf escale;                  // ES: per fold ‖C_f‖∞, then the row-sum scratch
   DBuf bfv;                       // sharded FITC block-LOO: row counts, then the fold values
   DBuf rpart;                     // per-workgroup partials of the row finalisers (main stream)
   size_t bL_zeroed = 0;
@@ -863,6 +864,7 @@ struct EsArgs {
   const double* draws = nullptr;  // device; fold f holds ξ_f then ξ'_f (S×b_f each, row-major)
   double lam_lb = 0.0;            // λmin(C_f) >= lam_lb; <= 0: unknown, iterate to ‖T − I‖ ≈ 0
   double diag_ub = 0.0;           // diag(C_f) <= diag_ub, so λmax <= b·diag_ub
+  double scale = 0.0;             // > 0: λmax(C_f) <= scale (‖C_f‖∞, full_blockloo), used instead
 };
 
 // Scaled Newton–Schulz schedule for a spectrum of C/s inside [x0, 1] (round 4).  The eigenvalue x
@@ -920,7 +922,10 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   const bool grad = G != nullptr;
   const int nmat = grad ? 10 : 5;
   const bool bounded = es.lam_lb > 0.0;
-  const double sc = bounded ? (double)b * es.diag_ub : trace_c;
+  // the scale s of C/s: ‖C_f‖∞ when the caller measured it (round 4: on C2's folds ~1.1 against
+  // the trace bound b(sf² + σ²) ≈ 1262, which left the spectrum of C/s three decades below 1 and
+  // cost the scaled schedule ~6 more steps), else the trace bound
+  const double sc = bounded ? (es.scale > 0.0 ? es.scale : (double)b * es.diag_ub) : trace_c;
   // β per step (ns_schedule); adaptive mode (no spectral bounds) runs unscaled steps
   const std::vector<double> beta = bounded ? ns_schedule(es.lam_lb / sc) : std::vector<double>(200, 1.0);
   const int iters = (int)beta.size();
@@ -1108,6 +1113,10 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   // products each) run concurrently, fold f on stream f mod 4 with its own work area;
   // C_f, r_f, w_f are kept per fold (the fold gradients land in disjoint blocks: full GP)
   const bool es_conc = esq && ctx->overlap && nfold > 1;
+  // ES with spectral bounds: ‖C_f‖∞ per fold scales the Newton–Schulz iteration (es_fold)
+  const bool es_norm = esq && es->lam_lb > 0.0;
+  if (es_norm) HIPCHK(ensure(ctx, ctx->escale, (size_t)(nfold + bp) * 8));
+  std::vector<double> hscale(nfold, 0.0);
   double *PIs = nullptr, *RW = nullptr;
   if (es_conc) {
     HIPCHK(ensure(ctx, ctx->bPIs, (size_t)nfold * bp * bp * 8));
@@ -1140,6 +1149,13 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
       if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
       HIPCHK(launch_sym_mirror(PI, bp, (int)bp, s));
     }
+    if (es_norm) {
+      HIPCHK(launch_norm_inf(PI, bp, (int)b, ctx->escale.d() + nfold, ctx->escale.d() + f, s));
+      if (!es_conc) {  // (serial folds: the fold's own bound before its iteration)
+        HIPCHK(hipMemcpyAsync(&hscale[f], ctx->escale.d() + f, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+      }
+    }
     if (es_conc) {  // r_f for the concurrent pass below
       HIPCHK(hipMemcpyAsync(RW + (int64_t)2 * f * bp, r, (size_t)bp * 8, hipMemcpyDeviceToDevice,
                             s));
@@ -1153,7 +1169,9 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
       ldg = dst.second;
     }
     if (esq) {
-      if ((rc = es_fold(ctx, s, ctx->ebuf, false, *es, es->draws + 2 * (int64_t)es->S * a, b, bp, ctx->bPI.d(), r, 0.0,
+      EsArgs ef = *es;
+      ef.scale = hscale[f] * (1.0 + 1e-12);
+      if ((rc = es_fold(ctx, s, ctx->ebuf, false, ef, es->draws + 2 * (int64_t)es->S * a, b, bp, ctx->bPI.d(), r, 0.0,
                         w, G, ldg, want_grad ? g + a : nullptr, fs + 3 * f + 2)))
         return rc;
     } else if (!kc) {  // DSS: G_f = −½(P⁻¹ + r rᵀ), g_f = r
@@ -1171,6 +1189,10 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
     if (want_grad && (rc = gdone(f, a, b))) return rc;
   }
   if (es_conc) {
+    if (es_norm) {  // every fold's ‖C_f‖∞ on the host before the schedules are cut
+      HIPCHK(hipMemcpyAsync(hscale.data(), ctx->escale.d(), (size_t)nfold * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
     hipStream_t st[4] = {s, ctx->side, ctx->aux[0], ctx->aux[1]};
     DBuf* eb[4] = {&ctx->ebuf, &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2]};
     const int nst = std::min(nfold, 4);
@@ -1188,7 +1210,9 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
         ldg = dst.second;
       }
       double* rf = RW + (int64_t)2 * f * bp;
-      if ((rc = es_fold(ctx, st[f % 4], *eb[f % 4], true, *es, es->draws + 2 * (int64_t)es->S * a, b,
+      EsArgs ef = *es;
+      ef.scale = hscale[f] * (1.0 + 1e-12);
+      if ((rc = es_fold(ctx, st[f % 4], *eb[f % 4], true, ef, es->draws + 2 * (int64_t)es->S * a, b,
                         bp, PIs + (int64_t)f * bp * bp, rf, 0.0, rf + bp, G, ldg,
                         want_grad ? g + a : nullptr, fs + 3 * f + 2)))
         return rc;
@@ -1232,7 +1256,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
                  &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt};
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->escale, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt};
 }
 
 extern "C" {

@@ -340,6 +340,9 @@ hipError_t launch_loo_grad_terms(const double* y, const double* alpha, const dou
                                  int n_pad, int obj, double* u, double* ct, hipStream_t s);
 // strictly-upper 32-tiles := transpose of the strictly-lower ones
 hipError_t launch_sym_mirror(double* M, int64_t ld, int n_pad, hipStream_t s);
+// *out = max_i Σ_j |A_ij| over the n×n block (the ∞-norm; rowsum: n doubles of scratch)
+hipError_t launch_norm_inf(const double* A, int64_t lda, int n, double* rowsum, double* out,
+                           hipStream_t s);
 int grad_contract_passes(int d);
 int64_t grad_contract_slab_doubles(int n, int d);
 // out[pass*18 + q]: q = 0 Σ w m K, 1 Σ_diag m, 2+k Σ w m K Δ²_(16·pass+k)

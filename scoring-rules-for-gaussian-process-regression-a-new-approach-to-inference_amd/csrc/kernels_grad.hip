@@ -88,6 +88,42 @@ hipError_t launch_sym_mirror(double* M, int64_t ld, int n_pad, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ∞-norm of a symmetric n×n block, an upper bound of its spectral radius (the energy score's
+// Newton–Schulz scale): one wave per row (coalesced), fixed-order lane sums, then one block
+// takes the max (order-free)
+__global__ __launch_bounds__(256) void row_abs_sum_kernel(const double* __restrict__ A, int64_t lda,
+                                                          int n, double* __restrict__ rowsum) {
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const double* row = A + (int64_t)r * lda;
+  double s = 0.0;
+  for (int j = lane; j < n; j += 64) s += fabs(row[j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) rowsum[r] = s;
+}
+__global__ __launch_bounds__(256) void max_kernel(const double* __restrict__ v, int n,
+                                                  double* __restrict__ out) {
+  __shared__ double red[256];
+  double m = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmax(m, v[i]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
+}
+hipError_t launch_norm_inf(const double* A, int64_t lda, int n, double* rowsum, double* out,
+                           hipStream_t s) {
+  if (n < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_abs_sum_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, A, lda, n,
+                     rowsum);
+  hipLaunchKernelGGL(max_kernel, dim3(1), dim3(256), 0, s, rowsum, n, out);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- contraction
 // One workgroup per lower 64×64 tile of the REAL n×n region; thread (rg, col) handles
 // column col and rows rg, rg+4, …, rg+60.  Per element:
