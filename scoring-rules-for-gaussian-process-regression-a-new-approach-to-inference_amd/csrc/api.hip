@@ -970,17 +970,20 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   // off-diagonal blocks of the gradient pass are Fréchet derivatives of those polynomials
   // in the symmetric direction Ḡ: every product (or pair sum) below is symmetric, so it
   // is formed on the lower tiles only (half the flops) and mirrored.
-  auto sym = [&](const double* A, const double* B, double* C, double alpha, double beta) {
+  // (mirror: the product completes C, whose strictly-lower 32-tiles then go above the diagonal
+  //  in the same launch sequence — GemmParams::mirror — instead of a sym_mirror launch after it)
+  auto sym = [&](const double* A, const double* B, double* C, double alpha, double beta,
+                 bool mirror = false) {
     GemmParams p = gp0();
     p.A = A; p.lda = bp; p.B = B; p.ldb = bp; p.C = C; p.ldc = bp;
     p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.alpha = alpha; p.beta = beta; p.lower_out = 1;
+    p.mirror = mirror ? 1 : 0;
     if (conc) {  // 4 folds in flight: 2 K slices of 64-tiles (C2 ES: ks 1/2/3/4/auto(8) =
       p.tile = 64;  // 54.8 / 53.9 / 54.4 / 55.3 / 58.5 ms per iteration)
       p.ksplit = 2;
     }
     return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p, s);
   };
-  auto mirror = [&](double* C) { return launch_sym_mirror(C, bp, (int)bp, s); };
   HIPCHK(launch_pad_copy(xi_src, b, xi, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
   HIPCHK(launch_pad_copy(xi_src + (int64_t)S * b, b, xip, bp, S, (int)b, (int)Sp, (int)bp, 0, s));
   double *Y = stored ? Ys[0] : M[0], *Z = stored ? Zk[0] : M[1], *T = M[2], *Yn = M[3],
@@ -995,19 +998,16 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
       Zn = Zk[it + 1];
     }
     const double bt = beta[it], mu = std::sqrt(bt);
-    if ((rc = sym(Z, Y, T, -0.5 * bt, 0.0))) return rc;
+    if ((rc = sym(Z, Y, T, -0.5 * bt, 0.0, true))) return rc;
     HIPCHK(launch_diag_add_const(T, bp, (int)bp, 1.5, s));
-    HIPCHK(mirror(T));
     if (!bounded && extra < 0) {  // ‖T − I‖²_F = ‖I − ZY‖²_F / 4
       HIPCHK(launch_ns_resid(T, bp, (int)bp, res, s));
       HIPCHK(hipMemcpyAsync(ctx->hsmall, res, 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       if (ctx->hsmall[0] < 1e-24 * (double)bp) extra = 3;
     }
-    if ((rc = sym(Y, T, Yn, mu, 0.0))) return rc;
-    HIPCHK(mirror(Yn));
-    if ((rc = sym(T, Z, Zn, mu, 0.0))) return rc;
-    HIPCHK(mirror(Zn));
+    if ((rc = sym(Y, T, Yn, mu, 0.0, true))) return rc;
+    if ((rc = sym(T, Z, Zn, mu, 0.0, true))) return rc;
     std::swap(Y, Yn);
     std::swap(Z, Zn);
     ++used;
@@ -1052,24 +1052,18 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
       Zkk = Zk[it];
       Tk = Ts[it];
     } else {
-      if ((rc = sym(Z1, Y1, T1, -0.5 * bt, 0.0))) return rc;
+      if ((rc = sym(Z1, Y1, T1, -0.5 * bt, 0.0, true))) return rc;
       HIPCHK(launch_diag_add_const(T1, bp, (int)bp, 1.5, s));
-      HIPCHK(mirror(T1));
     }
     if ((rc = sym(Zkk, Y2, T2, -0.5 * bt, 0.0))) return rc;  // T2 = −½β(Z1Y2 + Z2Y1)
-    if ((rc = sym(Z2, Yk, T2, -0.5 * bt, 1.0))) return rc;
-    HIPCHK(mirror(T2));
+    if ((rc = sym(Z2, Yk, T2, -0.5 * bt, 1.0, true))) return rc;
     if ((rc = sym(Yk, T2, Y2n, mu, 0.0))) return rc;   // Y2 ← √β(Y1T2 + Y2T1)
-    if ((rc = sym(Y2, Tk, Y2n, mu, 1.0))) return rc;
-    HIPCHK(mirror(Y2n));
+    if ((rc = sym(Y2, Tk, Y2n, mu, 1.0, true))) return rc;
     if ((rc = sym(Tk, Z2, Z2n, mu, 0.0))) return rc;   // Z2 ← √β(T1Z2 + T2Z1)
-    if ((rc = sym(T2, Zkk, Z2n, mu, 1.0))) return rc;
-    HIPCHK(mirror(Z2n));
+    if ((rc = sym(T2, Zkk, Z2n, mu, 1.0, true))) return rc;
     if (!stored) {
-      if ((rc = sym(Y1, T1, Y1n, mu, 0.0))) return rc;
-      HIPCHK(mirror(Y1n));
-      if ((rc = sym(T1, Z1, Z1n, mu, 0.0))) return rc;
-      HIPCHK(mirror(Z1n));
+      if ((rc = sym(Y1, T1, Y1n, mu, 0.0, true))) return rc;
+      if ((rc = sym(T1, Z1, Z1n, mu, 0.0, true))) return rc;
       std::swap(Y1, Y1n);
       std::swap(Z1, Z1n);
     }

@@ -75,6 +75,9 @@ struct GemmParams {
   // set by launch_gemm for the stream-K tail: tiles [sk_dp, tiles) are split over sk_wgs blocks
   int sk_dp, sk_wgs;
   int prio;                  // 1: the mainloop's MFMA phase at raised wave priority (g_gemm_prio)
+  int mirror;                // lower_out square launch: also write the strictly-lower 32-tiles'
+                             // transposes above the diagonal (a symmetric result, in the split-K
+                             // reduction when there is one, else by launch_sym_mirror)
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark

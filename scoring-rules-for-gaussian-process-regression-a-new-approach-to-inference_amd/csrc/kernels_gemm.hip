@@ -754,9 +754,42 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const double* __rest
   *c = v;
 }
 
+// The split-K reduction of a symmetric result (GemmParams::mirror): per lower 32-tile (r >= c)
+// the slices summed in order (the values splitk_reduce_kernel writes), the tile stored and, below
+// the diagonal, its transpose through LDS into tile (c, r) — sym_mirror's copy without a launch
+// (the energy score's Newton–Schulz chains: one launch fewer per product).
+__global__ __launch_bounds__(256) void splitk_reduce_sym_kernel(const double* __restrict__ ws, int ks,
+                                                                int N, double alpha, double beta,
+                                                                double* __restrict__ C, int64_t ldc) {
+  __shared__ double t[32][33];
+  const int b = blockIdx.x;
+  int r = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= b) ++r;
+  while (r * (r + 1) / 2 > b) --r;
+  const int c = b - r * (r + 1) / 2;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t slab = (int64_t)N * N;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = r * 32 + ty + 8 * k, j = c * 32 + tx;
+    const int64_t e = (int64_t)i * N + j;
+    double sum = ws[e];
+    for (int q = 1; q < ks; ++q) sum += ws[q * slab + e];
+    double v = alpha * sum;
+    double* cp = C + (int64_t)i * ldc + j;
+    if (beta != 0.0) v += beta * *cp;
+    *cp = v;
+    t[ty + 8 * k][tx] = v;
+  }
+  if (r == c) return;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) C[(int64_t)(c * 32 + ty + 8 * k) * ldc + r * 32 + tx] = t[tx][ty + 8 * k];
+}
+
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
-int g_gemm_glds = 0;
-int g_gemm_prio = 1;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
+int g_gemm_glds = 0;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
+int g_gemm_prio = 1;  // GPS_OPT_GEMM_PRIO (process-wide): s_setprio around the MFMA phase
 int g_stream_k = 0;   // GPS_OPT_STREAM_K (process-wide; off: DESIGN §6.20)
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
@@ -808,6 +841,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     return hipErrorInvalidValue;
   if ((p.lda & 1) || (p.ldb & 1) || (p.ldc & 1)) return hipErrorInvalidValue;
   if (p.lower_out && p.M != p.N) return hipErrorInvalidValue;
+  if (p.mirror && (!p.lower_out || p.M % 32)) return hipErrorInvalidValue;
   if (p.ksplit < 1) p.ksplit = 1;
   // the row dot comes from the last column tile, which must span the whole K range (columns
   // [tri_off, tri_off + N) of a larger triangular product whose last column is K)
@@ -836,6 +870,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     GPS_SMALL_LAYOUTS(2, 1) GPS_SMALL_LAYOUTS(2, 2) GPS_SMALL_LAYOUTS(2, 4)
 #undef GPS_SMALL_LAYOUTS
 #undef GPS_SMALL_CASE
+    if (err == hipSuccess && p.mirror) err = launch_sym_mirror(p.C, p.ldc, p.M, s);
     return err;
   }
   if (tile != 64 && tile != 128) return hipErrorInvalidValue;
@@ -919,7 +954,14 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   GPS_GEMM_CASE(LAY_T, LAY_N, EPI_STORE, 64)
   GPS_GEMM_CASE(LAY_T, LAY_T, EPI_STORE, 64)
 #undef GPS_GEMM_CASE
-  if (err != hipSuccess || !slabbed) return err;
+  if (err != hipSuccess) return err;
+  if (!slabbed) return p.mirror ? launch_sym_mirror(p.C, p.ldc, p.M, s) : hipSuccess;
+  if (p.mirror) {
+    const int64_t t32 = p.M / 32;
+    hipLaunchKernelGGL(splitk_reduce_sym_kernel, dim3((unsigned)(t32 * (t32 + 1) / 2)), dim3(256), 0,
+                       s, p.ws, p.ksplit, p.N, p.alpha, p.beta, p.C, p.ldc);
+    return hipGetLastError();
+  }
   const int64_t pairs = (int64_t)p.M * p.N / 2;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s,
                      p.ws, p.ksplit, p.M, p.N, p.lower_out ? tile : 0, p.alpha, p.beta, p.C, p.ldc);
