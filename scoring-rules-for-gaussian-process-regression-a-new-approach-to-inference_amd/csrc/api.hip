@@ -1140,8 +1140,8 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
       GemmParams p = gp0();
       p.A = ctx->bL.d(); p.lda = bp; p.B = ctx->bL.d(); p.ldb = bp; p.C = PI; p.ldc = bp;
       p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.tri = TRI_K_GE_I; p.lower_out = 1;
+      p.mirror = 1;
       if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
-      HIPCHK(launch_sym_mirror(PI, bp, (int)bp, s));
     }
     if (es_norm) {
       HIPCHK(launch_norm_inf(PI, bp, (int)b, ctx->escale.d() + nfold, ctx->escale.d() + f, s));
