@@ -1,5 +1,7 @@
 // Microbenchmark: v_mfma_f64_16x16x4_f64 issue rate / dependent latency on gfx950,
-// plus the fragment-map check (A = I, asymmetric B).  Build + run on the GPU box:
+// plus the fragment-map check (A = I, asymmetric B).
+// (Its rate column is event-timed over blocks the dispatcher may pack two to a CU, so it
+// reads ~2x slow; tools/mfma_f64_rate.hip measures per-wave cycles in-kernel: 64 per MFMA.)  Build + run on the GPU box:
 //   hipcc -O3 --offload-arch=gfx950 tools/mfma_f64_probe.hip -o /tmp/probe && /tmp/probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
