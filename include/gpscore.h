@@ -128,6 +128,10 @@ enum {
   GPS_OPT_GEMM_GLDS = 21, /* 1: 128-tile GEMM launches stage their operands global -> LDS directly
                              (global_load_lds) instead of through registers; 0 (default).  Same
                              values bitwise.  Process-wide. */
+  GPS_OPT_DAG_ORDER = 25, /* queue order of the persistent factorisation's tasks: 1 (default)
+                             largest upward rank with the round-4 measured task durations, 2 the
+                             same with round 3's, 0 earliest estimated start.  Same values bitwise
+                             (the order changes only which workgroup runs a task, and when). */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
@@ -147,7 +151,8 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
 /* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one
  * word per strip task (type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24; types 0 LEAF,
  * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN, 5 LEAF', 6 INV, 7 TRSM'; flags bit 0: the chain tasks' fine
- * parts (GPS_OPT_DAG_FINE), bit 1: the split chain (GPS_OPT_DAG_SPLIT) — kernels_potrf.hip).
+ * parts (GPS_OPT_DAG_FINE), bit 1: the split chain (GPS_OPT_DAG_SPLIT), bits 2-3: the order
+ * (GPS_OPT_DAG_ORDER: 0 or 1 the default 1, 2 order 2, 3 order 0) — kernels_potrf.hip).
  * Returns the queue length (writes at most cap words); needs no device. */
 int gps_dag_task_list(int T, int flags, uint32_t* out, int cap);
 

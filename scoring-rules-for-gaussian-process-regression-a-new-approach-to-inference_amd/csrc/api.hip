@@ -107,6 +107,7 @@ struct gps_ctx {
   int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: automatic, see dag_width)
   bool dag_fine = true;                // GPS_OPT_DAG_FINE
   bool dag_split = false;              // GPS_OPT_DAG_SPLIT
+  int dag_order = 1;                   // GPS_OPT_DAG_ORDER
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per 4T + 2 split + fine: device task list, length
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
@@ -446,7 +447,7 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
 
 // the task list of an nb-tile persistent block under the context's options
 int dag_list_key(const gps_ctx* ctx, int64_t nb) {
-  return (int)(4 * nb + 2 * (ctx->dag_split ? 1 : 0) + (ctx->dag_fine ? 1 : 0));
+  return (int)(4 * (3 * nb + ctx->dag_order) + 2 * (ctx->dag_split ? 1 : 0) + (ctx->dag_fine ? 1 : 0));
 }
 
 // a block of nb 128-tiles goes to the persistent factorisation (GPS_OPT_DAG)
@@ -623,7 +624,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   for (int T : dsizes) {
     const int lk = dag_list_key(ctx, T);
     if (ctx->dag_lists.count(lk)) continue;
-    const std::vector<uint32_t> tl = dag_task_list(T, 1, ctx->dag_fine, ctx->dag_split);
+    const std::vector<uint32_t> tl = dag_task_list(T, ctx->dag_order, ctx->dag_fine, ctx->dag_split);
     auto& e = ctx->dag_lists[lk];
     HIPCHK(ensure(ctx, e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
@@ -1376,6 +1377,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       return 0;
     case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
     case GPS_OPT_DAG_SPLIT: ctx->dag_split = value != 0; return 0;
+    case GPS_OPT_DAG_ORDER:
+      ARGCHK(value >= 0 && value <= 2, "GPS_OPT_DAG_ORDER must be 0, 1 or 2");
+      ctx->dag_order = value;
+      return 0;
     case GPS_OPT_DAG_GROUP:
       ARGCHK(value >= 2 && value <= 4, "GPS_OPT_DAG_GROUP must be 2, 3 or 4");
       ctx->dag_group = value;
@@ -1412,7 +1417,8 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
 
 int gps_dag_task_list(int T, int flags, uint32_t* out, int cap) {
   if (T < 2 || T > 64 || cap < 0 || (cap > 0 && !out)) return fail(nullptr, -1, "bad arguments");
-  const std::vector<uint32_t> tl = dag_task_list(T, 1, (flags & 1) != 0, (flags & 2) != 0);
+  const std::vector<uint32_t> tl = dag_task_list(T, (flags >> 2 & 3) == 0 ? 1 : (flags >> 2 & 3) == 3 ? 0 : flags >> 2 & 3,
+                                                 (flags & 1) != 0, (flags & 2) != 0);
   for (int i = 0; i < cap && i < (int)tl.size(); ++i) out[i] = tl[i];
   return (int)tl.size();
 }

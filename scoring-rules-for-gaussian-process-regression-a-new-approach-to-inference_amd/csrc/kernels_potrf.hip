@@ -1158,9 +1158,10 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
 //   order 0: earliest estimated start first (a forward critical-path pass; estimated µs: leaf 36,
 //            strip task 4, hand-off 3) — round 3's first build;
 //   order 1: largest upward rank first (the longest estimated path from the task to the end of
-//            the block, leaf 38, strip 9, hand-off 1: the durations the r3 trace measured), so the
-//            updates that feed the next leaves overtake the bulk of the trailing update (the first
-//            leaves waited 20-26 µs behind it).
+//            the block, with per-type durations), so the updates that feed the next leaves
+//            overtake the bulk of the trailing update (the first leaves waited 20-26 µs behind
+//            it), with the durations the round-4 traces measured (below);
+//   order 2: the same with round 3's weights (leaf 38, strip 9, fine part 4, hand-off 1).
 // fine: the leaf chain's TRSM(k+1,k) and UPD(k+1,k+1,k) as fine parts (8 / 16, see run_fine).
 // split: the chain without the leaf's inverse — LEAF'(k) (type 5: L_kk and the X_pp), INV(k)
 // (type 6: X_kk, off the chain), TRSM'(k+1,k) (type 7, 2 parts: substitution with L_kk and the
@@ -1211,13 +1212,36 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
     auto dur = [&](const Task& t) { return t.type == 0 || t.type == 5 ? 36.0 : 4.0; };
     for (int t = 0; t < n; ++t)  // generation order is topological
       for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
-  } else {
+  } else if (order == 2) {  // round 3's weights
     auto dur = [&](const Task& t) {
       return t.type == 0 ? 38.0 : t.type == 5 ? 27.0 : t.type == 6 ? 10.0 : is_fine(t) ? 4.0 : 9.0;
     };
-    for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
+    for (int t = n - 1; t >= 0; --t) {
       double m = 0.0;
       for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + 1.0);
+      tk[t].rank = dur(tk[t]) + m;
+      tk[t].est = -tk[t].rank;
+    }
+  } else {
+    // run time per strip task as the round-4 trace measured it (profiles/r4_dag_trace20_*.txt);
+    // the fine parts count 6 (they run 8.5 but 8-16 of them in parallel) and each hand-off 2.5
+    // (profiles/r4_dag_order_ab.txt: 3.6 % off the block against the round-3 weights)
+    auto dur = [&](const Task& t) {
+      if (is_fine(t)) return 6.0;
+      switch (t.type) {
+        case 0: return 35.0;
+        case 1: return 9.7;
+        case 2: return 11.7;
+        case 3: return 11.2;
+        case 4: return 9.3;
+        case 5: return 39.0;
+        case 6: return 14.0;
+        default: return 21.0;
+      }
+    };
+    for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
+      double m = 0.0;
+      for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + 2.5);
       tk[t].rank = dur(tk[t]) + m;
       tk[t].est = -tk[t].rank;  // smallest key first
     }

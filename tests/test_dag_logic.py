@@ -18,12 +18,12 @@ U = 16   # arrivals per finished tile task (dag::U)
 B = 8    # emulated tile edge (the device uses 128; the algebra is edge-independent)
 
 
-def task_list(T, fine=1, split=0):
-    """Queue words decoded as (type, part, i, j, k, fine)."""
+def task_list(T, fine=1, split=0, order=1):
+    """Queue words decoded as (type, part, i, j, k, fine); order as GPS_OPT_DAG_ORDER."""
     import ctypes
     from gpscore import _lib
     lib = _lib.load()
-    flags = fine | (split << 1)
+    flags = fine | (split << 1) | ({0: 3, 1: 1, 2: 2}[order] << 2)
     n = lib.gps_dag_task_list(T, flags, None, 0)
     assert n > 0
     out = (ctypes.c_uint32 * n)()
@@ -156,11 +156,12 @@ def check(em, A):
     assert np.allclose(X, np.linalg.inv(Lr), rtol=1e-11, atol=1e-11)
 
 
+@pytest.mark.parametrize("order", [0, 1, 2])
 @pytest.mark.parametrize("split", [0, 1])
 @pytest.mark.parametrize("fine", [0, 1])
 @pytest.mark.parametrize("T", [2, 3, 5, 8, 13])
-def test_queue_order_is_topological(T, fine, split):
-    tl = task_list(T, fine, split)
+def test_queue_order_is_topological(T, fine, split, order):
+    tl = task_list(T, fine, split, order)
     A = spd(T, T)
     em = Emu(A, T)
     for t in tl:
@@ -195,6 +196,15 @@ def test_counters_cover_every_dependency(T, seed, fine, split):
         assert ready, "deadlock"
         em.run(pending.pop(int(rng.choice(ready))))
     check(em, A)
+
+
+@pytest.mark.parametrize("T", [5, 20])
+def test_orders_queue_the_same_tasks(T):
+    """The orders differ only in sequence: same strip multiset, and they do differ."""
+    lists = [task_list(T, 1, 0, o) for o in (0, 1, 2)]
+    assert sorted(lists[0]) == sorted(lists[1]) == sorted(lists[2])
+    assert lists[1] != lists[2] and lists[1] != lists[0]
+    assert task_list(T, 1, 0) == lists[1]  # the default
 
 
 def test_queue_sizes():

@@ -876,3 +876,36 @@ def test_persistent_split_chain(gpu_ctx, n, tiles):
         assert abs(r1.objectives[k] - r0.objectives[k]) <= 1e-11 * max(1.0, abs(r0.objectives[k])), k
     f = O.fast_full_fit(X, y, *th)
     assert nrel(r1.mu_loo, f["loo_mu"]) < 1e-9 and nrel(r1.var_loo, f["loo_var"]) < 1e-9
+
+
+@pytest.mark.parametrize("n,tiles", [(2560, 20), (4000, 40)])
+def test_persistent_queue_orders_bitwise(gpu_ctx, n, tiles):
+    """GPS_OPT_DAG_ORDER: the queue order moves tasks between workgroups and in time, never the
+    arithmetic (every tile's update terms accumulate in k order through the arrival counters), so
+    orders 0, 1 (default) and 2 give the same bits; the default also against the oracle.
+    Reference: torch.potrf KF:26 / KF:332."""
+    import gpscore
+    from gpscore import _lib
+    rng = np.random.default_rng(n + 11)
+    d = 4
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((200, d))
+    y, yt = np.sin(X.sum(1)) + 0.1 * rng.standard_normal(n), np.sin(Xt.sum(1))
+    th = (0.0, np.log(1.3) * np.ones(d), np.log(0.05))
+    gp = gpscore.GP(ctx=gpu_ctx)
+    runs = []
+    try:
+        gpu_ctx.set_dag(True, tiles)
+        for order in (1, 2, 0):
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_ORDER, order)
+            r = gp.fit(X, y, th)
+            mu, var = gp.predict(Xt, yt)
+            runs.append((r, mu, var))
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_DAG_ORDER, 1)
+        gpu_ctx.set_dag(True, 20)
+    r1, mu1, var1 = runs[0]
+    for r, mu, var in runs[1:]:
+        assert r.objectives == r1.objectives and np.array_equal(mu, mu1) and np.array_equal(var, var1)
+        assert np.array_equal(r.mu_loo, r1.mu_loo) and np.array_equal(r.var_loo, r1.var_loo)
+    f = O.fast_full_fit(X, y, *th)
+    assert nrel(r1.mu_loo, f["loo_mu"]) < 1e-9 and nrel(r1.var_loo, f["loo_var"]) < 1e-9
