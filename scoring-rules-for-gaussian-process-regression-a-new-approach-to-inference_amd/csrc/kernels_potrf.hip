@@ -1167,6 +1167,10 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
 // (type 6: X_kk, off the chain), TRSM'(k+1,k) (type 7, 2 parts: substitution with L_kk and the
 // X_pp); the other TRSM(i,k) and the inverse tasks take X_kk from INV(k).
 // Word: type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24.
+// order 1's weights, µs: LEAF, fine part, TRSM, UPD, UPDX, FIN strips, hand-off (tools/dag_bench
+// overrides them for sweeps; the library never writes them)
+double g_dag_weights[7] = {35.0, 6.0, 9.7, 11.7, 11.2, 9.3, 2.5};
+
 std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
   struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0, rank = 0.0; };
   auto is_fine = [&](const Task& t) {
@@ -1226,14 +1230,15 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
     // run time per strip task as the round-4 trace measured it (profiles/r4_dag_trace20_*.txt);
     // the fine parts count 6 (they run 8.5 but 8-16 of them in parallel) and each hand-off 2.5
     // (profiles/r4_dag_order_ab.txt: 3.6 % off the block against the round-3 weights)
+    const double* w = g_dag_weights;
     auto dur = [&](const Task& t) {
-      if (is_fine(t)) return 6.0;
+      if (is_fine(t)) return w[1];
       switch (t.type) {
-        case 0: return 35.0;
-        case 1: return 9.7;
-        case 2: return 11.7;
-        case 3: return 11.2;
-        case 4: return 9.3;
+        case 0: return w[0];
+        case 1: return w[2];
+        case 2: return w[3];
+        case 3: return w[4];
+        case 4: return w[5];
         case 5: return 39.0;
         case 6: return 14.0;
         default: return 21.0;
@@ -1241,7 +1246,7 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
     };
     for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
       double m = 0.0;
-      for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + 2.5);
+      for (int s2 : succ[t]) m = std::max(m, tk[s2].rank + w[6]);
       tk[t].rank = dur(tk[t]) + m;
       tk[t].est = -tk[t].rank;  // smallest key first
     }

@@ -26,6 +26,13 @@ int main(int argc, char** argv) {
   const int order = argc > 6 ? atoi(argv[6]) : 1;
   const int fine = argc > 7 ? atoi(argv[7]) : 1;
   const int split = argc > 8 ? atoi(argv[8]) : 0;
+  if (argc > 9) {  // order 1's weights: LEAF,fine,TRSM,UPD,UPDX,FIN,hand-off
+    double* w = gps::g_dag_weights;
+    if (sscanf(argv[9], "%lf,%lf,%lf,%lf,%lf,%lf,%lf", w, w + 1, w + 2, w + 3, w + 4, w + 5, w + 6) != 7) {
+      fprintf(stderr, "weights: 7 comma-separated numbers\n");
+      return 2;
+    }
+  }
   const int n = 128 * T, d = 8;
   // SPD test block: ARD-style Gram of random points + noise (what the recursion hands down)
   std::mt19937_64 rng(7);
@@ -109,7 +116,7 @@ int main(int argc, char** argv) {
   double lsum = 0;
   for (double x : gld) lsum += x;
   const double fl = 2.0 * n * (double)n * n / 3.0;
-  printf("group=%d order=%d fine=%d split=%d ", group, order, fine, split);
+  printf("group=%d order=%d fine=%d split=%d w=%s ", group, order, fine, split, argc > 9 ? argv[9] : "-");
   printf("T=%d n=%d nwg=%d tasks=%d: median %.3f ms (min %.3f, max %.3f) = %.1f us/tile, %.2f TF/s; "
          "max|XAX^T - I| %.2e over 24 samples, sum log L_ii %.6f\n",
          T, n, nwg, nt, ts[ts.size() / 2], ts[0], ts.back(), 1e3 * ts[ts.size() / 2] / T,
