@@ -68,8 +68,8 @@ enum {
   GPS_OPT_OVERLAP = 0,  /* 1 (default): the factorisation's off-critical-path products (and the
                            energy score's folds) run on extra HIP streams; 0: everything on one
                            stream (clean per-kernel timing) */
-  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 fixed orders,
-                           6 automatic without the row-norm patch order (A/B) */
+  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 and 7 fixed
+                           orders, 6 / 8 automatic with the row norms in order 3 / 7 (A/B) */
   GPS_OPT_FORK_MIN = 4, /* smallest recursion block (in 128-row blocks, default 1) whose
                            off-critical-path product is forked to the side stream */
   GPS_OPT_TINY_GEMM = 7, /* 1 (default): the bottom-of-recursion GEMMs (up to the 1280 level)
@@ -128,6 +128,11 @@ enum {
   GPS_OPT_GEMM_GLDS = 21, /* 1: 128-tile GEMM launches stage their operands global -> LDS directly
                              (global_load_lds) instead of through registers; 0 (default).  Same
                              values bitwise.  Process-wide. */
+  GPS_OPT_SLAB_XCD = 26,  /* 1: split-K GEMM launches (the FITC SYRK, small trailing updates) deal
+                             their (tile, K slice) pairs slice-major, each XCD a contiguous run,
+                             so one XCD's resident workgroups share a slice's operand rows in its
+                             L2 (default; C4's SYRK 7x -> 2.9x its operand in L2-fabric bytes,
+                             time neutral); 0: tile-major.  Same values bitwise.  Process-wide. */
   GPS_OPT_DAG_ORDER = 25, /* queue order of the persistent factorisation's tasks: 1 (default)
                              largest upward rank with the round-4 measured task durations, 2 the
                              same with round 3's, 0 earliest estimated start.  Same values bitwise

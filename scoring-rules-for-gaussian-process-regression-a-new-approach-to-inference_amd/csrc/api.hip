@@ -656,7 +656,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
       (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->fork_max, (uintptr_t)ctx->gemm_map,
-      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)g_gemm_glds, (uintptr_t)g_gemm_prio, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
+      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)g_gemm_glds, (uintptr_t)g_gemm_prio, (uintptr_t)g_slab_xcd, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
       (uintptr_t)ctx->ws_side.p, (uintptr_t)pre,
       // the pre-pass's operands (only when it is part of the sequence)
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
@@ -1366,6 +1366,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_STREAM_K: g_stream_k = value != 0; return 0;
     case GPS_OPT_GEMM_GLDS: g_gemm_glds = value != 0; return 0;
+    case GPS_OPT_SLAB_XCD: g_slab_xcd = value != 0; return 0;
     case GPS_OPT_GEMM_PRIO: g_gemm_prio = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;

@@ -65,7 +65,8 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
                              // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto,
-                             // 5 XCD-banded 8×8 patches (auto for EPI_ROWSQ), 6 auto without 5
+                             // 5 XCD-banded 8×8 patches (auto for EPI_ROWSQ), 6 auto without 5,
+                             // 7 XCD-banded with the band index inner, 8 auto with 7 for EPI_ROWSQ
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
@@ -78,6 +79,8 @@ struct GemmParams {
   int mirror;                // lower_out square launch: also write the strictly-lower 32-tiles'
                              // transposes above the diagonal (a symmetric result, in the split-K
                              // reduction when there is one, else by launch_sym_mirror)
+  int slab_xcd;              // set by launch_gemm (g_slab_xcd): a split-K grid's (tile, slice)
+                             // pairs dealt slice-major in contiguous runs per XCD
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
@@ -88,6 +91,7 @@ extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kerne
 extern int g_stream_k;   // 1: the stream-K tail of uniform-K 128-tile launches (launch_gemm)
 extern int g_gemm_glds;  // 1: 128-tile launches stage operands global -> LDS directly (glds)
 extern int g_gemm_prio;  // s_setprio around the mainloop's MFMA phase: 0 off, 1 (default) products, 2 all
+extern int g_slab_xcd;   // split-K launches: each XCD runs whole K slices (GPS_OPT_SLAB_XCD)
 constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)
 
 // ------------------------------------------------------------ device reductions

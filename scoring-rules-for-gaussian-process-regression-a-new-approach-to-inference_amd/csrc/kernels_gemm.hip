@@ -87,6 +87,21 @@ __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int
     tj = p.tri == TRI_K_LE_J ? p.tiles_n - 1 - cj : cj;
     return ti < p.tiles_m && cj < p.tiles_n;
   }
+  if (p.map_mode == 7) {
+    // XCD-banded, band index inner (A/B): as map 3, XCD x owns a contiguous band of the index
+    // that does not carry the triangular work, but walks it panel by panel: the tiles of one
+    // band panel (every value of the work index, heaviest first) are consecutive, so they are
+    // co-resident and read that panel once from HBM into the XCD's L2
+    const int x = t & 7, i = t >> 3;
+    const bool wi = p.tri == TRI_K_LE_I || p.tri == TRI_K_GE_I;
+    const int nb = wi ? p.tiles_n : p.tiles_m, nw = wi ? p.tiles_m : p.tiles_n;
+    const int bb = (nb + 7) >> 3, bi = x * bb + i / nw, wk = i % nw;
+    if (bi >= nb || i / nw >= bb) return false;
+    const int widx = (p.tri == TRI_K_LE_I || p.tri == TRI_K_LE_J) ? nw - 1 - wk : wk;
+    ti = wi ? widx : bi;
+    tj = wi ? bi : widx;
+    return true;
+  }
   if (p.map_mode == 5) {
     // XCD-banded 8×8 patches (the automatic order of the FITC row norms): as map 3, XCD x owns
     // a band of the index that does not carry the triangular work, but its resident tiles form 8 (band) × 8
@@ -145,8 +160,18 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       return;
     }
   }
-  const int nblk = p.sk_wgs > 0 ? p.sk_dp : (int)gridDim.x;
   int ti, tj;
+  if (p.slab_xcd) {
+    // split-K, slice-major per XCD: the grid's (tile, slice) pairs in slice-major order, each XCD
+    // a contiguous run of them, so the workgroups resident on an XCD share one K slice's rows of
+    // both operands in its L2 (the tile-major remap spreads an XCD over every slice)
+    const int nt = (int)gridDim.x;
+    const int l = xcd_remap((int)(blockIdx.x + blockIdx.y * gridDim.x), nt * (int)gridDim.y);
+    if (!tile_of(p, l % nt, ti, tj)) return;
+    gemm_tile<ALAY, BLAY, EPI, TILE, GL>(p, ti, tj, l / nt, smem);
+    return;
+  }
+  const int nblk = p.sk_wgs > 0 ? p.sk_dp : (int)gridDim.x;
   if (!tile_of(p, remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x, ti, tj)) return;
   gemm_tile<ALAY, BLAY, EPI, TILE, GL>(p, ti, tj, blockIdx.y, smem);
 }
@@ -790,6 +815,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_sym_kernel(const double* __
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
 int g_gemm_glds = 0;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
 int g_gemm_prio = 1;  // GPS_OPT_GEMM_PRIO (process-wide): s_setprio around the MFMA phase
+// GPS_OPT_SLAB_XCD (process-wide): split-K launches slice-major per XCD.  The FITC SYRK's L2-fabric
+// bytes 4.48 -> 1.91 GB per C4 launch (7x -> 2.9x its Knm operand), time neutral (C4 11.86 -> 11.83,
+// C3 / C5 within noise: profiles/r4_slab_xcd_ab.txt) — the SYRK is not fabric-bound
+int g_slab_xcd = 1;
 int g_stream_k = 0;   // GPS_OPT_STREAM_K (process-wide; off: DESIGN §6.20)
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
@@ -896,16 +925,24 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build; the
   // FITC row norms (EPI_ROWSQ) to its 8×8-patch form (map 5): C5 174.0 vs 181.5 ms, while the
   // patch order on the factorisation / predictive TRMMs cost C3 27 % (profiles/r2_map5_ab.txt)
-  const bool rowsq_patch = q.map_mode != 6;  // 6: the automatic order without it (A/B runs)
-  if (q.map_mode == 6) q.map_mode = 0;
+  // 6 / 8: the automatic order with map 3 / 7 for the row norms (A/B runs; both slower in the
+  // library on C4 or C5: profiles/r4_rowsq_map_ab.txt)
+  const int rowsq_map = q.map_mode == 6 ? 3 : q.map_mode == 8 ? 7 : 5;
+  if (q.map_mode == 6 || q.map_mode == 8) q.map_mode = 0;
   if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out)
-    q.map_mode = (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) && rowsq_patch ? 5 : 3;
+    q.map_mode = (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) ? rowsq_map : 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
   if (q.map_mode == 5 && (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J)) q.map_mode = 0;
   if (q.map_mode == 5) {  // 8 XCDs × ceil(work / 8) groups × the band's 8-wide groups × 64
     const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;
     const int nb = wi ? q.tiles_n : q.tiles_m, nw = wi ? q.tiles_m : q.tiles_n;
     tiles = 8 * ((nw + 7) / 8) * (((nb + 7) / 8 + 7) / 8) * 64;
+  }
+  if (q.map_mode == 7) {
+    if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
+    const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;
+    const int nb = wi ? q.tiles_n : q.tiles_m, nw = wi ? q.tiles_m : q.tiles_n;
+    tiles = 8 * ((nb + 7) / 8) * nw;
   }
   if (q.map_mode == 3) {
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
@@ -929,6 +966,9 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // raised MFMA-phase priority: 1 = the product / column-reduction launches only (C3 −1.3 %;
   // the FITC row-norm launches and the Λ-scaled SYRK ran 0.4 % slower with it), 2 = every launch
   q.prio = g_gemm_prio == 2 || (g_gemm_prio == 1 && (epi == EPI_STORE || epi == EPI_COLRED) && !q.kscale);
+  // slice-major per XCD: split-K launches whose tile index is the plain (or remapped) raster
+  q.slab_xcd = g_slab_xcd && q.ksplit > 1 && q.sk_wgs == 0 &&
+               (q.map_mode == 0 || q.map_mode == 2) && (q.lower_out || q.tri == TRI_NONE);
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
   // direct-to-LDS staging (GPS_OPT_GEMM_GLDS): 128-tiles without a per-k operand scale, the

@@ -30,6 +30,7 @@ GPS_OPT_DAG_FINE = 22
 GPS_OPT_DAG_SPLIT = 23
 GPS_OPT_GEMM_PRIO = 24
 GPS_OPT_DAG_ORDER = 25
+GPS_OPT_SLAB_XCD = 26
 GPS_OPT_FORK_MAX = 14
 GPS_OPT_AR_CHUNKS = 15
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")

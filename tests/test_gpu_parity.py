@@ -803,6 +803,7 @@ def test_persistent_factorisation_potrf_exports(gpu_ctx):
 
 def test_gemm_glds_bitwise(gpu_ctx):
     """GPS_OPT_GEMM_GLDS (direct global -> LDS operand staging in the 128-tile GEMM)
+    and GPS_OPT_SLAB_XCD (split-K slices per XCD)
     computes every product with the same fragments in the same k order as register staging: the
     full-GP fit + predict (NT / NN / TN products, SYRKs, the fused predictive column reductions)
     and the FITC fit + predict + gradient (row-norm epilogues, Woodbury products) are bitwise
@@ -834,6 +835,15 @@ def test_gemm_glds_bitwise(gpu_ctx):
     finally:
         gpu_ctx.call("gps_ctx_set_option", 21, 0)
     for a, b in zip(gl, base):
+        assert np.array_equal(a, b)
+    # GPS_OPT_SLAB_XCD (26): split-K launches dealt slice-major per XCD — only which workgroup
+    # runs a (tile, slice) pair changes, the slabs and their ordered sum do not
+    try:
+        gpu_ctx.call("gps_ctx_set_option", 26, 0)
+        sx = run()
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", 26, 1)
+    for a, b in zip(sx, base):
         assert np.array_equal(a, b)
 
 

@@ -14,6 +14,9 @@ import gpscore  # noqa: E402
 c = bench.CONFIGS["C4"]
 X, y, Xt, yt, Z, th = bench.synth(c["n"], c["d"], c["nt"], c["seed"], c["m"])
 gp = gpscore.GP()
+if os.environ.get("GPS_SLAB_XCD"):  # A/B of GPS_OPT_SLAB_XCD under the counter passes
+    from gpscore import _lib
+    gp.ctx.call("gps_ctx_set_option", _lib.GPS_OPT_SLAB_XCD, int(os.environ["GPS_SLAB_XCD"]))
 gp.set_data(X, y, kind="fitc", Z=Z)
 gp.set_test(Xt, yt)
 for _ in range(2):

@@ -250,10 +250,10 @@ static int layout_study(double* A, double* B, double* C) {
 static int rowsq_study(double* A, double* B, double* o0) {
   struct S { const char* name; int M, N; } cs[] = {
     {"C4 fit  40064x2048", 40064, 2048}, {"C4 pred 10112x2048", 10112, 2048},
-    {"C5/2    100032x4096", 100032, 4096}};
+    {"C5/2    100096x4096", 100096, 4096}};
   GemmParams p; memset(&p, 0, sizeof(p));
   for (auto& c : cs)
-    for (int mm = 0; mm < 4; ++mm) {
+    for (int mm : {0, 6, 7, 1}) {  // auto (5), 3, 7, grouped raster
       p.A = A; p.B = B; p.out0 = o0; p.alpha = 1.0; p.ksplit = 1; p.tile = 0;
       p.lda = c.N; p.ldb = c.N; p.ld_out = c.M;
       p.M = c.M; p.N = c.N; p.K = c.N; p.tri = TRI_K_LE_J; p.map_mode = mm;
@@ -263,11 +263,41 @@ static int rowsq_study(double* A, double* B, double* o0) {
   return 0;
 }
 
+// FITC split-K SYRK B = Kmnᵀ diag(λ⁻¹) Knm at the C4 / C5 shapes: the library's TN form (Knm
+// row-major n×m, A transposed) against the NT form over a stored Kmn = Knmᵀ (m×n), with and
+// without the per-k scale, and slice-major per XCD (g_slab_xcd)
+static int fsyrk_study(double* A, double* C, double* w) {
+  double* ws;
+  if (hipMalloc(&ws, (int64_t)24 * 4096 * 4096 * 8) != hipSuccess) return 1;
+  hipLaunchKernelGGL(fill_rand, dim3(64), dim3(256), 0, 0, w, (int64_t)200064, 3ull);
+  // (operands: A holds n*n = 419M doubles; 4096 x 100032 = 410M fit)
+  struct S { const char* name; int m, n, ks; } cs[] = {{"C4 2048 K=40064", 2048, 40064, 11},
+                                                       {"C5/2 4096 K=100032", 4096, 100032, 13}};
+  GemmParams p; memset(&p, 0, sizeof(p));
+  for (auto& c : cs)
+    for (int lay = 0; lay < 2; ++lay)
+      for (int ksc = 0; ksc < 2; ++ksc)
+        for (int sx = 0; sx < 2; ++sx) {
+          memset(&p, 0, sizeof(p));
+          p.A = A; p.B = A; p.C = C; p.ws = ws; p.ws_cap = (int64_t)24 * 4096 * 4096;
+          p.M = c.m; p.N = c.m; p.K = c.n; p.lower_out = 1; p.ksplit = c.ks; p.alpha = 1.0; p.ldc = c.m;
+          p.kscale = ksc ? w : nullptr;
+          const int al = lay == 0 ? LAY_T : LAY_N, bl = lay == 0 ? LAY_N : LAY_T;
+          p.lda = lay == 0 ? c.m : c.n; p.ldb = p.lda;
+          g_slab_xcd = sx;
+          const double fl = (double)c.m * (c.m + 1) * c.n;
+          printf("fsyrk %-18s %s kscale%d sxcd%d %7.2f TF/s\n", c.name, lay == 0 ? "TN" : "NT", ksc, sx,
+                 run(al, bl, EPI_STORE, p, 5, fl));
+        }
+  g_slab_xcd = 0;
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 20480;
   double *A, *B, *C, *o0, *o1, *w;
   hipMalloc(&A, n * n * 8); hipMalloc(&B, n * n * 8); hipMalloc(&C, n * n * 8);
-  hipMalloc(&o0, 64 * 200064 * 8); hipMalloc(&o1, 256 * n * 8); hipMalloc(&w, n * 8);
+  hipMalloc(&o0, 64 * 200064 * 8); hipMalloc(&o1, 256 * n * 8); hipMalloc(&w, 200064 * 8);
   const bool zeros = getenv("GB_ZEROS") != nullptr;
   if (zeros) { hipMemset(A, 0, n * n * 8); hipMemset(B, 0, n * n * 8); }
   else {
@@ -284,6 +314,7 @@ int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "syrk")) return syrk_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "layout")) return layout_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "rowsq")) return rowsq_study(A, B, o0);
+  if (argc > 1 && !strcmp(argv[1], "fsyrk")) return fsyrk_study(A, C, w);
   if (argc > 1 && !strcmp(argv[1], "sweep")) {
     double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);
     return sweep(A, B, C, ws);
