@@ -58,21 +58,6 @@ constexpr int GROUP_M = 8;
 // operands since the microbenchmark below) keeps that equal-work-per-XCD property
 // but gives each XCD a compact band of tiles: 70.7 TF/s on the same TRMM.
 __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int& tj) {
-  if (p.lower_out && p.map_mode == 10) {
-    // lower-triangle 8×8 patches (A/B): XCD x runs patches x, x + 8, ... of the triangle's patch
-    // grid (row-major lower patches), each patch's 64 tiles consecutive, so an XCD's resident
-    // tiles need 16 operand panels instead of ~65 for a run along one tile row.  Positions above
-    // the diagonal or past the edge are holes.
-    const int x = t & 7, i = t >> 3, P = x + 8 * (i >> 6), w = i & 63;
-    int r = (int)((sqrt(8.0 * (double)P + 1.0) - 1.0) * 0.5);
-    while ((r + 1) * (r + 2) / 2 <= P) ++r;
-    while (r * (r + 1) / 2 > P) --r;
-    const int pc = P - r * (r + 1) / 2, np = (p.tiles_m + 7) >> 3;
-    if (r >= np) return false;
-    ti = r * 8 + (w >> 3);
-    tj = pc * 8 + (w & 7);
-    return ti < p.tiles_m && tj <= ti;
-  }
   if (p.lower_out) {
     int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
     while ((r + 1) * (r + 2) / 2 <= t) ++r;
@@ -168,7 +153,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
   __shared__ __attribute__((aligned(16))) double smem[2 * STAGE];
   const bool remap = p.map_mode == 2 || (p.map_mode == 0 && p.tri == TRI_NONE);
-  // (map_mode 1 also disables the remap for lower-triangular SYRK grids; 10 has its own order)
+  // (map_mode 1 also disables the remap for lower-triangular SYRK grids)
   if constexpr (EPI == EPI_STORE && TILE == 128) {
     if (p.sk_wgs > 0 && (int)blockIdx.x >= p.sk_dp) {  // the stream-K tail (launch_gemm)
       gemm_sk_block<ALAY, BLAY>(p, (int)blockIdx.x - p.sk_dp, smem);
@@ -953,14 +938,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     const int nb = wi ? q.tiles_n : q.tiles_m, nw = wi ? q.tiles_m : q.tiles_n;
     tiles = 8 * ((nw + 7) / 8) * (((nb + 7) / 8 + 7) / 8) * 64;
   }
-  if (q.map_mode == 10) {  // lower-triangle 8×8 patches (tile_of)
-    if (!q.lower_out) {
-      q.map_mode = 0;
-    } else {
-      const int np = (q.tiles_m + 7) / 8, npatch = np * (np + 1) / 2;
-      tiles = 8 * ((npatch + 7) / 8) * 64;
-    }
-  }
   if (q.map_mode == 7) {
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
     const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;
@@ -977,8 +954,7 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // over every slot instead
   q.sk_dp = q.sk_wgs = 0;
   if (g_stream_k && epi == EPI_STORE && tile == 128 && q.ksplit == 1 && q.sk_cnt && q.ws &&
-      q.sk_slots > 0 && q.tri == TRI_NONE && q.map_mode != 10 &&
-      (q.lower_out || q.map_mode == 0 || q.map_mode == 2)) {
+      q.sk_slots > 0 && q.tri == TRI_NONE && (q.lower_out || q.map_mode == 0 || q.map_mode == 2)) {
     const int slots = q.sk_slots, rem = tiles % slots;
     if (tiles >= slots && rem > 0 && 4 * rem <= 3 * slots && rem <= kStreamKTiles &&
         (int64_t)(rem + slots) * 128 * 128 <= q.ws_cap && q.K / BK >= 2) {
