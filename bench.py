@@ -89,6 +89,11 @@ def spawn_ranks(n):
     import subprocess
     port = os.environ.get("MASTER_PORT") or str(_free_port())
     procs = []
+    stop = {"sig": None}
+
+    def on_signal(signum, _frame):  # the parent itself told to stop: the ranks go with it
+        stop["sig"] = signum
+    old_handlers = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT)}
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
@@ -99,6 +104,13 @@ def spawn_ranks(n):
     kill_at = None
     live = list(procs)
     while live:
+        if stop["sig"] is not None and kill_at is None:
+            print(f"[bench] spawner got signal {stop['sig']}; stopping the ranks", file=sys.stderr,
+                  flush=True)
+            rc = rc or 128 + stop["sig"]
+            for q in live:
+                q.send_signal(signal.SIGTERM)
+            kill_at = time.time() + 30.0
         for p in list(live):
             code = p.poll()
             if code is None:
@@ -114,8 +126,10 @@ def spawn_ranks(n):
         if kill_at is not None and time.time() > kill_at:
             for q in live:
                 q.kill()
-            kill_at = None
+            kill_at = float("inf")
         time.sleep(0.2)
+    for sg, h in old_handlers.items():
+        signal.signal(sg, h)
     return rc
 
 
@@ -156,6 +170,14 @@ class Ctl:
         t = torch.tensor([v], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t[0])
+
+    def gather(self, obj):
+        """every rank's `obj`, in rank order, on every rank (gloo object all-gather)"""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
 
 def sync_all(ctl, ctx):
@@ -398,6 +420,97 @@ def parity(got, ref):
     return out
 
 
+C5_FIXTURE = os.path.join(ROOT, "tests", "golden", "c5_n1_outputs.json")
+FITC_VECS = ("loo_mu", "loo_var", "pred_mu", "pred_var")
+
+
+def comm_check(ctl, world, rank, local, info, kind="rccl"):
+    """Every rank's communicator as the library reports it (gps_comm_info: RCCL's own
+    ncclCommCount / ncclCommUserRank), gathered over the control plane: the run's ranks agree
+    when each communicator counts `world` ranks of the expected kind and the user ranks are a
+    permutation of 0..world−1 equal to the launcher's RANKs."""
+    seen = ctl.gather([rank, local] + list(info))
+    agree = (all(n == world and k == kind for _, _, n, _, k in seen)
+             and sorted(ur for _, _, _, ur, _ in seen) == list(range(world))
+             and all(r == ur for r, _, _, ur, _ in seen))
+    return {"ranks_seen": sorted({n for _, _, n, _, _ in seen}), "all_ranks_agree": bool(agree),
+            "per_rank": [{"rank": r, "local_rank": lr, "comm_count": n, "comm_user_rank": ur,
+                          "kind": k} for r, lr, n, ur, k in seen]}
+
+
+def sample_indices(n):
+    """Global row indices whose values the C5 fixture keeps: 48 evenly spaced rows plus both
+    sides of every shard boundary of 2, 4 and 8 ranks (gpscore.dist.shard_rows), where an
+    off-by-one in the shard bookkeeping would show."""
+    from gpscore.dist import shard_rows
+    idx = set(int(i) for i in np.linspace(0, n - 1, 48))
+    for p in (2, 4, 8):
+        for r in range(1, p):
+            a, _ = shard_rows(n, p, r)
+            idx.update((a - 1, a))
+    return sorted(i for i in idx if 0 <= i < n)
+
+
+def fitc_outputs(ctl, fgp, thf, fc, rows, test_rows):
+    """The sharded C5 unit's outputs made rank-independent: the global objectives and test scores
+    (every rank holds them), and for each of LOO μ/σ² (rows) and predictive μ/σ² (test rows) the
+    all-rank sums Σv, Σv², Σ|v|, max|v| and the values at `sample_indices` — gathered over the gloo
+    control plane, so N ranks and one rank report the same quantities (K20:222-234, 270-296)."""
+    r = fgp.fit(theta=thf)
+    mu, var, sc = fgp.predict(with_scores=True)
+    local = {"loo_mu": (r.mu_loo, rows[0], fc["n"]), "loo_var": (r.var_loo, rows[0], fc["n"]),
+             "pred_mu": (mu, test_rows[0], fc["nt"]), "pred_var": (var, test_rows[0], fc["nt"])}
+    mine = {}
+    for k, (v, off, n) in local.items():
+        v = np.asarray(v, np.float64)
+        samp = {i: float(v[i - off]) for i in sample_indices(n) if off <= i < off + len(v)}
+        mine[k] = {"sum": float(v.sum()), "sumsq": float(v @ v), "sumabs": float(np.abs(v).sum()),
+                   "maxabs": float(np.abs(v).max()) if len(v) else 0.0, "count": int(len(v)),
+                   "samples": samp}
+    everyone = ctl.gather(mine)
+    vecs = {}
+    for k in FITC_VECS:
+        parts = [e[k] for e in everyone]
+        samples = {}
+        for p in parts:
+            samples.update(p["samples"])
+        vecs[k] = {"sum": float(sum(p["sum"] for p in parts)),
+                   "sumsq": float(sum(p["sumsq"] for p in parts)),
+                   "sumabs": float(sum(p["sumabs"] for p in parts)),
+                   "maxabs": max(p["maxabs"] for p in parts),
+                   "count": int(sum(p["count"] for p in parts)),
+                   "samples": {str(i): samples[i] for i in sorted(samples)}}
+    return {"objectives": dict(r.objectives), "scores": dict(sc), "vectors": vecs}
+
+
+def compare_fitc_outputs(got, ref):
+    """Errors of `got` against the committed N = 1 outputs `ref` (same quantities, fitc_outputs),
+    each as a normwise relative error: scalars |a − b| / max(1, |b|); sampled entries
+    max|a_i − b_i| / max|b|; Σv and Σ|v| relative to Σ|b|, Σv² to Σb².  The bar is the fixture's
+    `tol` (50·κ·ε at C5: the C5 tests' absolute cap, κ = cond(K̃mm)(sf² + σ²)/σ²)."""
+    errs = {}
+    for grp in ("objectives", "scores"):
+        for k, b in ref[grp].items():
+            errs[f"{grp}.{k}"] = abs(float(got[grp][k]) - b) / max(1.0, abs(b))
+    for k, rv in ref["vectors"].items():
+        gv = got["vectors"][k]
+        if gv["count"] != rv["count"] or set(gv["samples"]) != set(rv["samples"]):
+            errs[f"{k}.layout"] = float("inf")
+            continue
+        scale = max(rv["maxabs"], 1e-300)
+        errs[f"{k}.samples"] = max(abs(gv["samples"][i] - rv["samples"][i]) for i in rv["samples"]) / scale
+        errs[f"{k}.sum"] = abs(gv["sum"] - rv["sum"]) / max(rv["sumabs"], 1e-300)
+        errs[f"{k}.sumabs"] = abs(gv["sumabs"] - rv["sumabs"]) / max(rv["sumabs"], 1e-300)
+        errs[f"{k}.sumsq"] = abs(gv["sumsq"] - rv["sumsq"]) / max(rv["sumsq"], 1e-300)
+        errs[f"{k}.maxabs"] = abs(gv["maxabs"] - rv["maxabs"]) / scale
+    tol = float(ref["tol"])
+    worst = max(errs, key=lambda k: errs[k])
+    return {"vs": f"committed N = 1 outputs ({os.path.relpath(C5_FIXTURE, ROOT)}, "
+                  f"{ref.get('source', '')})",
+            "tol": tol, "max_err": errs[worst], "worst": worst, "ok": bool(errs[worst] <= tol),
+            "errors": errs}
+
+
 def gpu_unit_outputs(gp, th, rbf=False):
     r = gp.fit(theta=th, rbf=rbf)
     mu, var, sc = gp.predict(with_scores=True)
@@ -507,6 +620,25 @@ def fitc_cpu_baseline():
                              "unit — not the reference algorithm"}
 
 
+def c5_tol(Z, th):
+    """50·κ·ε, κ = cond(K̃mm)(sf² + σ²)/σ² from the host eigenvalues of the jittered K(Z, Z):
+    the absolute cap the C5 parity tests hold every output to (tests/test_gpu_parity.py
+    fitc_cap), stored with the fixture."""
+    O, _ = _oracle()
+    Kmm = O.fast_gram(Z, Z, th[0], th[1], diag_add=O.FITC_JITTER)
+    ev = np.linalg.eigvalsh(Kmm)
+    sf2, sn2 = np.exp(th[0]), np.exp(th[2])
+    return float(50.0 * (ev[-1] / ev[0]) * (sf2 + sn2) / sn2 * np.finfo(np.float64).eps)
+
+
+def host_gpu():
+    try:
+        import torch
+        return torch.cuda.get_device_name(0)
+    except Exception:  # noqa: BLE001
+        return "unknown device"
+
+
 def log(msg):
     """Progress on stderr (the JSON line alone goes to stdout): a long run keeps writing, so a
     watchdog that reads silence as a hang sees the legs go by."""
@@ -530,6 +662,10 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
                          "no RCCL communicator (FITC objectives then cover the local shard only)")
+    ap.add_argument("--write-c5-fixture", metavar="PATH", default=None,
+                    help="N = 1 only: write the C5 unit's rank-independent outputs (fitc_outputs) "
+                         "to PATH — the fixture tests/golden/c5_n1_outputs.json that N > 1 runs "
+                         "are checked against")
     ap.add_argument("--dry", action="store_true",
                     help="launcher / control-plane check: ranks meet over gloo, agree on the world "
                          "size and print the JSON skeleton without touching the GPU")
@@ -555,16 +691,29 @@ def main():
         if ctl.dist:
             everyone = [None] * world
             ctl.dist.all_gather_object(everyone, me)
+        if os.environ.get("GPS_BENCH_DRY_SLEEP"):  # launcher test: ranks that are still running
+            time.sleep(float(os.environ["GPS_BENCH_DRY_SLEEP"]))
+        # the rank-count check of the FITC leg, on a stand-in for gps_comm_info (no GPU here);
+        # GPS_BENCH_DRY_COMM_COUNT makes one rank's stand-in report a wrong count
+        bad = os.environ.get("GPS_BENCH_DRY_COMM_COUNT", "")
+        n_seen = int(bad.split(":")[1]) if bad and bad.split(":")[0] == str(rank) else world
+        rc = comm_check(ctl, world, rank, local, (n_seen, rank, "dry"), kind="dry")
         if rank == 0:
             ok = sorted(r for r, _, _ in everyone) == list(range(world)) and \
                 len({p for _, _, p in everyone}) == world
-            print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
-                              "ranks": everyone, "ranks_ok": ok, "steps": args.steps,
-                              "warmup": args.warmup}))
+            line = {"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
+                    "ranks": everyone, "ranks_ok": ok, "steps": args.steps,
+                    "warmup": args.warmup, "fitc": {"rccl": rc}}
+            if not rc["all_ranks_agree"]:
+                line["failures"] = [f"communicators disagree with --gpus {world}"]
+            print(json.dumps(line))
         if ctl.dist:
             ctl.dist.destroy_process_group()
+        if not rc["all_ranks_agree"]:
+            sys.exit(4)
         return
     import gpscore
+    failures = []  # self-checks that fail the run (non-zero exit) after the JSON line
     ctx = gpscore.Context(0 if args.rehearse else local)
     if args.no_tiny_gemm:
         ctx.set_tiny_gemm(False)
@@ -687,8 +836,10 @@ def main():
                 uid = buf.raw
             obj_l = [uid]
             ctl.dist.broadcast_object_list(obj_l, src=0)
+            info = None
             try:
                 ctx.call("gps_comm_init", world, rank, ctypes.create_string_buffer(obj_l[0], 128))
+                info = ctx.comm_info()
             except Exception as e:  # noqa: BLE001 - reported in the JSON line, not fatal
                 comm_err = repr(e)
             # every rank learns whether any communicator failed (over gloo, so no rank is
@@ -696,6 +847,12 @@ def main():
             if ctl.max(1.0 if comm_err else 0.0) > 0:
                 legs = []
                 fitc["error"] = comm_err or "gps_comm_init failed on another rank"
+            else:
+                fitc["rccl"] = comm_check(ctl, world, rank, local, info)
+                if not fitc["rccl"]["all_ranks_agree"]:
+                    failures.append(f"RCCL communicators disagree with --gpus {world}: "
+                                    f"{fitc['rccl']['per_rank']}")
+                    legs = []
         for leg in legs:
             fc = CONFIGS[leg]
             Xf, yf, Xtf, ytf, Z, thf = synth(fc["n"], fc["d"], fc["nt"], fc["seed"], fc["m"])
@@ -716,6 +873,9 @@ def main():
             fprof, fms_acct = kernel_pass(ctl, ctx, funit, args.steps)
             fphases = phases(ctl, ctx, fgp, thf, args.steps, fprof, 1e3 * tf / args.steps)
             fobj = fgp.fit(theta=thf, return_loo=False).objectives
+            fout = None
+            if leg == "C5" and not args.rehearse:  # outside the timed passes
+                fout = fitc_outputs(ctl, fgp, thf, fc, (a, b), (ta, tb))
             fitc[leg] = {"ms_per_step": 1e3 * tf / args.steps,
                          "units_per_s": args.steps / tf,
                          "config": {"n": fc["n"], "m": fc["m"], "d": fc["d"], "n_test": fc["nt"],
@@ -728,6 +888,24 @@ def main():
                          "kernel_accounting_ms_per_step": fms_acct,
                          "phases": fphases,
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
+            if fout is not None:
+                if args.write_c5_fixture and world == 1 and rank == 0:
+                    fixture = dict(fout, config=dict(fc), theta=[thf[0], list(thf[1]), thf[2]],
+                                   tol=c5_tol(Z, thf), source=f"bench.py N = 1 on {host_gpu()}")
+                    with open(args.write_c5_fixture, "w") as f:
+                        json.dump(fixture, f, indent=1, sort_keys=True)
+                    log(f"C5 fixture written to {args.write_c5_fixture}")
+                if os.path.exists(C5_FIXTURE):
+                    with open(C5_FIXTURE) as f:
+                        cmp = compare_fitc_outputs(fout, json.load(f))
+                    fitc[leg]["parity_vs_n1"] = cmp
+                    if not cmp["ok"]:
+                        failures.append(f"C5 at N = {world} differs from the N = 1 fixture: "
+                                        f"{cmp['worst']} {cmp['max_err']:.3g} > {cmp['tol']:.3g}")
+                else:
+                    fitc[leg]["parity_vs_n1"] = {"error": f"{C5_FIXTURE} missing"}
+                    if world > 1:
+                        failures.append("no N = 1 fixture to check the sharded C5 unit against")
             if not args.no_grad:  # next-1: one FITC GD iteration (theta and Z), K20:222-247
                 fg = {}
                 for objective in ("nlml", "loo_crps"):
@@ -766,10 +944,16 @@ def main():
             res["fitc"]["C4"]["cpu_baseline"] = fitc_cpu_baseline()
     if args.rehearse:
         res["rehearsal"] = "all ranks on device 0, no RCCL: not a measurement"
+    if failures:
+        res["failures"] = failures
     if rank == 0:
         print(json.dumps(res))
     if ctl.dist:
         ctl.dist.destroy_process_group()
+    if failures:  # the line is printed (it carries the evidence), but the run fails
+        for f in failures:
+            print(f"[bench] FAILED: {f}", file=sys.stderr, flush=True)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

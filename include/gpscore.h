@@ -51,7 +51,15 @@ enum {
 };
 
 /* ---- context ------------------------------------------------------------ */
+/* ABI version of this header; gps_version() returns the library's.  Bumped whenever an entry
+ * point changes its arguments or an array it writes changes size (500: gps_ctx_stats takes a
+ * capacity, gps_comm_info and gps_build_id added).  The binding refuses a mismatch at load. */
+#define GPS_ABI_VERSION 500
 int gps_version(void);
+/* The SHA-256 (hex) of the sources the library was built from (csrc/, this header; computed by
+ * gpscore/buildid.py at build time).  Writes at most cap-1 characters and a NUL; returns the
+ * id's length. */
+int gps_build_id(char* out, int cap);
 int gps_ctx_create(int device, gps_ctx** out);
 int gps_ctx_destroy(gps_ctx* ctx);
 const char* gps_last_error(gps_ctx* ctx);
@@ -68,8 +76,8 @@ enum {
   GPS_OPT_OVERLAP = 0,  /* 1 (default): the factorisation's off-critical-path products (and the
                            energy score's folds) run on extra HIP streams; 0: everything on one
                            stream (clean per-kernel timing) */
-  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 and 7 fixed
-                           orders, 6 / 8 automatic with the row norms in order 3 / 7 (A/B) */
+  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 fixed orders
+                           (A/B measurements; same values bitwise) */
   GPS_OPT_FORK_MIN = 4, /* smallest recursion block (in 128-row blocks, default 1) whose
                            off-critical-path product is forked to the side stream */
   GPS_OPT_TINY_GEMM = 7, /* 1 (default): the bottom-of-recursion GEMMs (up to the 1280 level)
@@ -121,13 +129,6 @@ enum {
                              column-reduction launches (C3 −1.1 %), 2 for every launch (the FITC
                              row-norm and Λ-scaled SYRK launches ran 0.4 % slower), 0 off.  Same
                              values.  Process-wide. */
-  GPS_OPT_DAG_SPLIT = 23, /* 1: the persistent factorisation's chain without the leaf's inverse —
-                             LEAF' factors and inverts only the 16×16 diagonal blocks, TRSM(k+1,k)
-                             substitutes with them, an INV task forms L_kk⁻¹ off the chain;
-                             0 (default): the leaf forms L_kk and L_kk⁻¹ together. */
-  GPS_OPT_GEMM_GLDS = 21, /* 1: 128-tile GEMM launches stage their operands global -> LDS directly
-                             (global_load_lds) instead of through registers; 0 (default).  Same
-                             values bitwise.  Process-wide. */
   GPS_OPT_SLAB_XCD = 26,  /* 1: split-K GEMM launches (the FITC SYRK, small trailing updates) deal
                              their (tile, K slice) pairs slice-major, each XCD a contiguous run,
                              so one XCD's resident workgroups share a slice's operand rows in its
@@ -151,14 +152,15 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 enum { GPS_STAT_GRAPHS = 0, GPS_STAT_GRAPH_CAP = 1, GPS_STAT_GRAPH_OVERFLOW = 2,
        GPS_STAT_DEVICE_BYTES = 3, GPS_STAT_GRAPH_DROPPED = 4, GPS_STAT_GRAPH_EVICTED = 5,
        GPS_N_STATS = 6 };
-int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]);
+/* Writes min(cap, GPS_N_STATS) entries; returns GPS_N_STATS (the count this library knows). */
+int gps_ctx_stats(gps_ctx* ctx, int64_t* out, int cap);
 
 /* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one
  * word per strip task (type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24; types 0 LEAF,
- * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN, 5 LEAF', 6 INV, 7 TRSM'; flags bit 0: the chain tasks' fine
- * parts (GPS_OPT_DAG_FINE), bit 1: the split chain (GPS_OPT_DAG_SPLIT), bits 2-3: the order
- * (GPS_OPT_DAG_ORDER: 0 or 1 the default 1, 2 order 2, 3 order 0) — kernels_potrf.hip).
- * Returns the queue length (writes at most cap words); needs no device. */
+ * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN; flags bit 0: the chain tasks' fine parts (GPS_OPT_DAG_FINE),
+ * bits 2-3: the order (GPS_OPT_DAG_ORDER: 0 or 1 the default 1, 2 order 2, 3 order 0), other
+ * bits rejected — kernels_potrf.hip).  Returns the queue length (writes at most cap words);
+ * needs no device. */
 int gps_dag_task_list(int T, int flags, uint32_t* out, int cap);
 
 /* on: 0 off, 1 per-kernel-class tags, 2 GEMM tags also carry layout/shape/tri/split-K/lda */
@@ -302,6 +304,11 @@ int gps_comm_init(gps_ctx* ctx, int nranks, int rank, const char uid[128]);
  * gps_comm_init_local again, which joins a fresh group under the same key).  Two live
  * contexts may not hold the same rank of one group. */
 int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group);
+/* What the context's communicator holds: *nranks and *rank as RCCL reports them
+ * (ncclCommCount / ncclCommUserRank) for GPS_COMM_RCCL, the group's size and this context's rank
+ * for GPS_COMM_LOCAL, 1 and 0 with GPS_COMM_NONE. */
+enum { GPS_COMM_NONE = 0, GPS_COMM_RCCL = 1, GPS_COMM_LOCAL = 2 };
+int gps_comm_info(gps_ctx* ctx, int* nranks, int* rank, int* kind);
 /* Leaves either communicator. */
 int gps_comm_destroy(gps_ctx* ctx);
 

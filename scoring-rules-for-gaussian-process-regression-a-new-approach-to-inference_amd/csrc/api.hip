@@ -106,10 +106,13 @@ struct gps_ctx {
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
   int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: automatic, see dag_width)
   bool dag_fine = true;                // GPS_OPT_DAG_FINE
-  bool dag_split = false;              // GPS_OPT_DAG_SPLIT
   int dag_order = 1;                   // GPS_OPT_DAG_ORDER
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
-  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 4T + 2 split + fine: device task list, length
+  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2(3T + order) + fine: device task list, length
+  // factor buffers (L⁻¹, L) known to hold zeros for a padded size: potrf_inv writes their lower
+  // triangles only and refuses a buffer without an entry here (zero_factor); freeing or growing
+  // a buffer forgets its entries (the zero-upper contract is checked, not assumed)
+  std::map<uintptr_t, int64_t> zeroed;
   DBuf dag_cnt;                        // arrival counters of every persistent launch of a call
   DBuf sk_cnt;                         // stream-K tail tickets of the main stream's GEMMs (zero)
   int64_t dag_cnt_used = 0;
@@ -144,7 +147,6 @@ struct gps_ctx {
   // ---- full GP state
   DBuf X, y, Xt, yt, A, Linv, W, logdiag, beta, alpha, dinv, slab, mu_loo, var_loo, Ksf, s1, s2,
       mu, var, Lout, pslab;
-  size_t linv_zeroed = 0;
   int n_ell = 1;
   DBuf gu, gct, gv, Mx, gslab, gout;  // gradient scratch
   int64_t n = 0, n_pad = 0, nt = 0, nt_pad = 0;
@@ -163,8 +165,6 @@ struct gps_ctx {
   DBuf escale;                  // ES: per fold ‖C_f‖∞, then the row-sum scratch
   DBuf bfv;                       // sharded FITC block-LOO: row counts, then the fold values
   DBuf rpart;                     // per-workgroup partials of the row finalisers (main stream)
-  size_t bL_zeroed = 0;
-  size_t lm_zeroed = 0, lb_zeroed = 0;
   int64_t fn = 0, fn_pad = 0, fnt = 0, fnt_pad = 0, m = 0, m_pad = 0, fn_total = 0, fnt_total = 0;
   int fd = 0;
   double f_ytr_mean = 0, f_ytr_var = 1;
@@ -252,10 +252,17 @@ hipError_t drop_graphs_in(gps_ctx* ctx, const void* p, size_t bytes) {
   return hipSuccess;
 }
 
+void forget_zeroed(gps_ctx* ctx, const void* p, size_t bytes) {
+  const uintptr_t lo = (uintptr_t)p, hi = lo + bytes;
+  for (auto it = ctx->zeroed.lower_bound(lo); it != ctx->zeroed.end() && it->first < hi;)
+    it = ctx->zeroed.erase(it);
+}
+
 hipError_t ensure(gps_ctx* ctx, DBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return hipSuccess;
   if (b.p) {
+    forget_zeroed(ctx, b.p, b.cap);
     hipError_t e = drop_graphs_in(ctx, b.p, b.cap);
     if (e != hipSuccess) return e;
     e = hipFree(b.p);
@@ -269,6 +276,7 @@ hipError_t ensure(gps_ctx* ctx, DBuf& b, size_t bytes) {
 }
 void release(gps_ctx* ctx, DBuf& b) {
   if (b.p) {
+    forget_zeroed(ctx, b.p, b.cap);
     (void)drop_graphs_in(ctx, b.p, b.cap);
     (void)hipFree(b.p);
   }
@@ -447,7 +455,7 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
 
 // the task list of an nb-tile persistent block under the context's options
 int dag_list_key(const gps_ctx* ctx, int64_t nb) {
-  return (int)(4 * (3 * nb + ctx->dag_order) + 2 * (ctx->dag_split ? 1 : 0) + (ctx->dag_fine ? 1 : 0));
+  return (int)(2 * (3 * nb + ctx->dag_order) + (ctx->dag_fine ? 1 : 0));
 }
 
 // a block of nb 128-tiles goes to the persistent factorisation (GPS_OPT_DAG)
@@ -497,7 +505,6 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     d.cnt = static_cast<int*>(ctx->dag_cnt.p) + ctx->dag_cnt_used;
     d.spin_ticks = 200000000ull;  // 2 s at the 100 MHz real-time clock
     d.group = ctx->dag_group;
-    d.split = ctx->dag_split ? 1 : 0;
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
@@ -609,8 +616,23 @@ int reset_info(gps_ctx* ctx) {  // [first non-PD minor, persistent-kernel error]
 // eager path remains for profiling (per-launch events) and as the option's off state.
 constexpr size_t kMaxGraphs = 64;
 
+// an n_pad × n_pad factor buffer at p, zeroed (stream-ordered on s) and recorded for potrf_inv
+hipError_t zero_factor(gps_ctx* ctx, double* p, int64_t n_pad, hipStream_t s) {
+  const hipError_t e = hipMemsetAsync(p, 0, (size_t)n_pad * n_pad * 8, s);
+  if (e == hipSuccess) ctx->zeroed[(uintptr_t)p] = n_pad;
+  return e;
+}
+bool factor_zeroed(const gps_ctx* ctx, const double* p, int64_t n_pad) {
+  const auto it = ctx->zeroed.find((uintptr_t)p);
+  return it != ctx->zeroed.end() && it->second == n_pad;
+}
+
 int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, double* logdiag,
               int nreal, double* Lout) {
+  // the leaves and strip tasks write the lower triangles only: the strict-upper 128-tiles of
+  // Linv / Lout must already be zero for THIS layout (n_pad is the row stride)
+  if (!factor_zeroed(ctx, Linv, n_pad) || (Lout && !factor_zeroed(ctx, Lout, n_pad)))
+    return fail(ctx, -1, "potrf_inv: factor buffer not zeroed for this size (internal contract)");
   // persistent blocks: task lists per size (uploaded once, before any capture) and one counter
   // region per launch of this call.  The regions are zero when a launch starts: zeroed once when
   // the buffer is allocated (synchronously, outside any capture) and reset by each launch's last
@@ -624,7 +646,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   for (int T : dsizes) {
     const int lk = dag_list_key(ctx, T);
     if (ctx->dag_lists.count(lk)) continue;
-    const std::vector<uint32_t> tl = dag_task_list(T, ctx->dag_order, ctx->dag_fine, ctx->dag_split);
+    const std::vector<uint32_t> tl = dag_task_list(T, ctx->dag_order, ctx->dag_fine);
     auto& e = ctx->dag_lists[lk];
     HIPCHK(ensure(ctx, e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
@@ -656,7 +678,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
       (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->fork_max, (uintptr_t)ctx->gemm_map,
-      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)g_gemm_glds, (uintptr_t)g_gemm_prio, (uintptr_t)g_slab_xcd, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
+      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)g_gemm_prio, (uintptr_t)g_slab_xcd, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
       (uintptr_t)ctx->ws_side.p, (uintptr_t)pre,
       // the pre-pass's operands (only when it is part of the sequence)
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
@@ -1088,10 +1110,9 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   const int nfold = (int)bnd.size() - 1;
   const int64_t bp = bounds_pad(bnd);
   HIPCHK(ensure(ctx, ctx->bP, (size_t)bp * bp * 8));
-  if (ctx->bL.cap < (size_t)bp * bp * 8 || ctx->bL_zeroed != (size_t)bp) {
+  if (ctx->bL.cap < (size_t)bp * bp * 8 || !factor_zeroed(ctx, ctx->bL.d(), bp)) {
     HIPCHK(ensure(ctx, ctx->bL, (size_t)bp * bp * 8));
-    HIPCHK(hipMemsetAsync(ctx->bL.p, 0, (size_t)bp * bp * 8, s));
-    ctx->bL_zeroed = (size_t)bp;
+    HIPCHK(zero_factor(ctx, ctx->bL.d(), bp, s));
   }
   HIPCHK(ensure(ctx, ctx->bPI, (size_t)bp * bp * 8));
   HIPCHK(ensure(ctx, ctx->bH, (size_t)bp * bp * 8));
@@ -1104,12 +1125,15 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
          *gm = v + 5 * bp, *gc = v + 6 * bp, *w = v + 7 * bp, *yf = v + 8 * bp;
   double* fs = v + 9 * bp;  // per fold: [Σ log L_ii, α·r, kc / es]
   const bool kc = objective == GPS_BLOCK_KC, esq = objective == GPS_BLOCK_ES;
-  // ES with the overlap option: the folds' square roots (hundreds of latency-bound b×b
-  // products each) run concurrently, fold f on stream f mod 4 with its own work area;
-  // C_f, r_f, w_f are kept per fold (the fold gradients land in disjoint blocks: full GP)
-  const bool es_conc = esq && ctx->overlap && nfold > 1;
   // ES with spectral bounds: ‖C_f‖∞ per fold scales the Newton–Schulz iteration (es_fold)
   const bool es_norm = esq && es->lam_lb > 0.0;
+  // ES in two passes — every fold's C_f and r_f first, then the square roots — whenever the folds
+  // can run concurrently (the overlap option: fold f on stream f mod 4 with its own work area) or
+  // their schedules need ‖C_f‖∞: the bounds of all folds then come back in ONE host read instead
+  // of a stream drain per fold.  C_f, r_f, w_f are kept per fold (the fold gradients
+  // land in disjoint blocks: full GP).
+  const int es_streams = ctx->overlap ? (int)std::min<int64_t>(nfold, 4) : 1;
+  const bool es_conc = esq && (es_streams > 1 || es_norm);
   if (es_norm) HIPCHK(ensure(ctx, ctx->escale, (size_t)(nfold + bp) * 8));
   std::vector<double> hscale(nfold, 0.0);
   double *PIs = nullptr, *RW = nullptr;
@@ -1144,14 +1168,9 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
       p.mirror = 1;
       if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
     }
-    if (es_norm) {
+    if (es_norm)
       HIPCHK(launch_norm_inf(PI, bp, (int)b, ctx->escale.d() + nfold, ctx->escale.d() + f, s));
-      if (!es_conc) {  // (serial folds: the fold's own bound before its iteration)
-        HIPCHK(hipMemcpyAsync(&hscale[f], ctx->escale.d() + f, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-      }
-    }
-    if (es_conc) {  // r_f for the concurrent pass below
+    if (es_conc) {  // r_f for the second pass below
       HIPCHK(hipMemcpyAsync(RW + (int64_t)2 * f * bp, r, (size_t)bp * 8, hipMemcpyDeviceToDevice,
                             s));
       continue;
@@ -1190,7 +1209,7 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
     }
     hipStream_t st[4] = {s, ctx->side, ctx->aux[0], ctx->aux[1]};
     DBuf* eb[4] = {&ctx->ebuf, &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2]};
-    const int nst = std::min(nfold, 4);
+    const int nst = es_streams;
     hipEvent_t fork = sync_event(ctx);
     if (!fork) return fail(ctx, -2, "hipEventCreate failed");
     HIPCHK(hipEventRecord(fork, s));
@@ -1207,7 +1226,7 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
       double* rf = RW + (int64_t)2 * f * bp;
       EsArgs ef = *es;
       ef.scale = hscale[f] * (1.0 + 1e-12);
-      if ((rc = es_fold(ctx, st[f % 4], *eb[f % 4], true, ef, es->draws + 2 * (int64_t)es->S * a, b,
+      if ((rc = es_fold(ctx, st[f % nst], *eb[f % nst], nst > 1, ef, es->draws + 2 * (int64_t)es->S * a, b,
                         bp, PIs + (int64_t)f * bp * bp, rf, 0.0, rf + bp, G, ldg,
                         want_grad ? g + a : nullptr, fs + 3 * f + 2)))
         return rc;
@@ -1256,7 +1275,8 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
 
 extern "C" {
 
-int gps_version(void) { return 100; }
+int gps_version(void) { return GPS_ABI_VERSION; }
+
 
 // the off-critical-path streams: side (T products of the factorisation) and aux[0..1]
 // (with side, the concurrent energy-score folds)
@@ -1339,7 +1359,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
   if (int rc = bind(ctx)) return rc;
   switch (key) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
-    case GPS_OPT_GEMM_MAP: ctx->gemm_map = value; return 0;
+    case GPS_OPT_GEMM_MAP:
+      ARGCHK(value >= 0 && value <= 5, "GPS_OPT_GEMM_MAP must be in 0..5");
+      ctx->gemm_map = value;
+      return 0;
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
     case GPS_OPT_FORK_MAX: ctx->fork_max = value < 0 ? 0 : value; return 0;
     case GPS_OPT_SIDE_PRIO: {  // the side stream at the lowest queue priority (or back)
@@ -1365,7 +1388,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
     case GPS_OPT_STREAM_K: g_stream_k = value != 0; return 0;
-    case GPS_OPT_GEMM_GLDS: g_gemm_glds = value != 0; return 0;
     case GPS_OPT_SLAB_XCD: g_slab_xcd = value != 0; return 0;
     case GPS_OPT_GEMM_PRIO: g_gemm_prio = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
@@ -1377,7 +1399,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->dag_wgs = value;
       return 0;
     case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
-    case GPS_OPT_DAG_SPLIT: ctx->dag_split = value != 0; return 0;
     case GPS_OPT_DAG_ORDER:
       ARGCHK(value >= 0 && value <= 2, "GPS_OPT_DAG_ORDER must be 0, 1 or 2");
       ctx->dag_order = value;
@@ -1402,24 +1423,27 @@ int gps_ctx_synchronize(gps_ctx* ctx) {
   return 0;
 }
 
-int gps_ctx_stats(gps_ctx* ctx, int64_t out[GPS_N_STATS]) {
+int gps_ctx_stats(gps_ctx* ctx, int64_t* out, int cap) {
   if (int rc = bind(ctx)) return rc;
-  ARGCHK(out != nullptr, "out is NULL");
+  ARGCHK(out != nullptr && cap >= 0, "out is NULL or cap < 0");
   size_t bytes = 0;
   for (DBuf* b : ctx_buffers(ctx)) bytes += b->cap;
-  out[GPS_STAT_GRAPHS] = (int64_t)ctx->pgraphs.size();
-  out[GPS_STAT_GRAPH_CAP] = (int64_t)kMaxGraphs;
-  out[GPS_STAT_GRAPH_OVERFLOW] = ctx->graph_overflow;
-  out[GPS_STAT_GRAPH_DROPPED] = ctx->graph_dropped;
-  out[GPS_STAT_GRAPH_EVICTED] = ctx->graph_evicted;
-  out[GPS_STAT_DEVICE_BYTES] = (int64_t)bytes;
-  return 0;
+  int64_t v[GPS_N_STATS];
+  v[GPS_STAT_GRAPHS] = (int64_t)ctx->pgraphs.size();
+  v[GPS_STAT_GRAPH_CAP] = (int64_t)kMaxGraphs;
+  v[GPS_STAT_GRAPH_OVERFLOW] = ctx->graph_overflow;
+  v[GPS_STAT_GRAPH_DROPPED] = ctx->graph_dropped;
+  v[GPS_STAT_GRAPH_EVICTED] = ctx->graph_evicted;
+  v[GPS_STAT_DEVICE_BYTES] = (int64_t)bytes;
+  for (int i = 0; i < cap && i < GPS_N_STATS; ++i) out[i] = v[i];  // never past the caller's array
+  return GPS_N_STATS;
 }
 
 int gps_dag_task_list(int T, int flags, uint32_t* out, int cap) {
-  if (T < 2 || T > 64 || cap < 0 || (cap > 0 && !out)) return fail(nullptr, -1, "bad arguments");
+  if (T < 2 || T > 64 || cap < 0 || (cap > 0 && !out) || (flags & ~13))
+    return fail(nullptr, -1, "bad arguments");
   const std::vector<uint32_t> tl = dag_task_list(T, (flags >> 2 & 3) == 0 ? 1 : (flags >> 2 & 3) == 3 ? 0 : flags >> 2 & 3,
-                                                 (flags & 1) != 0, (flags & 2) != 0);
+                                                 (flags & 1) != 0);
   for (int i = 0; i < cap && i < (int)tl.size(); ++i) out[i] = tl[i];
   return (int)tl.size();
 }
@@ -1500,12 +1524,12 @@ static int factor_user(gps_ctx* ctx, int64_t n, const double* A, int64_t lda, bo
   HIPCHK(launch_pad_copy(ctx->t0.d(), lda, ctx->t1.d(), np, (int)n, (int)n, (int)np, (int)np, 1,
                          ctx->stream));
   HIPCHK(ensure(ctx, ctx->t2, (size_t)np * np * 8));
-  HIPCHK(hipMemsetAsync(ctx->t2.p, 0, (size_t)np * np * 8, ctx->stream));  // L⁻¹ upper tiles = 0
+  HIPCHK(zero_factor(ctx, ctx->t2.d(), np, ctx->stream));  // L⁻¹ upper tiles = 0
   HIPCHK(ensure(ctx, ctx->t3, potrf_ws_doubles(np) * 8));
   HIPCHK(ensure(ctx, ctx->t4, (size_t)np * 8 * (want_L ? np + 1 : 1)));
   double* logdiag = ctx->t4.d();
   double* Lout = want_L ? ctx->t4.d() + np : nullptr;
-  if (want_L) HIPCHK(hipMemsetAsync(Lout, 0, (size_t)np * np * 8, ctx->stream));
+  if (want_L) HIPCHK(zero_factor(ctx, Lout, np, ctx->stream));
   if (int rc = reset_info(ctx)) return rc;
   if (int rc = potrf_inv(ctx, ctx->t1.d(), np, ctx->t2.d(), ctx->t3.d(), logdiag, (int)n, Lout))
     return rc;
@@ -1682,10 +1706,9 @@ int full_fit_core(gps_ctx* ctx, int kind, const double* theta, int n_ell) {
   const int64_t n = ctx->n, np = ctx->n_pad;
   hipStream_t s = ctx->stream;
   HIPCHK(ensure(ctx, ctx->A, (size_t)np * np * 8));
-  if (ctx->Linv.cap < (size_t)np * np * 8 || ctx->linv_zeroed != (size_t)np) {
+  if (ctx->Linv.cap < (size_t)np * np * 8 || !factor_zeroed(ctx, ctx->Linv.d(), np)) {
     HIPCHK(ensure(ctx, ctx->Linv, (size_t)np * np * 8));
-    HIPCHK(hipMemsetAsync(ctx->Linv.p, 0, (size_t)np * np * 8, s));
-    ctx->linv_zeroed = (size_t)np;
+    HIPCHK(zero_factor(ctx, ctx->Linv.d(), np, s));
   }
   HIPCHK(ensure(ctx, ctx->W, potrf_ws_doubles(np) * 8));
   HIPCHK(ensure(ctx, ctx->logdiag, np * 8));
@@ -2114,12 +2137,12 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   // buffers
   HIPCHK(ensure(ctx, ctx->Kmm, (size_t)mp * mp * 8));
   HIPCHK(ensure(ctx, ctx->Am, (size_t)mp * mp * 8));
-  if (ctx->lm_zeroed != (size_t)mp || ctx->Lm.cap < (size_t)mp * mp * 8) {
+  if (ctx->Lm.cap < (size_t)mp * mp * 8 || ctx->Lb.cap < (size_t)mp * mp * 8 ||
+      !factor_zeroed(ctx, ctx->Lm.d(), mp) || !factor_zeroed(ctx, ctx->Lb.d(), mp)) {
     HIPCHK(ensure(ctx, ctx->Lm, (size_t)mp * mp * 8));
     HIPCHK(ensure(ctx, ctx->Lb, (size_t)mp * mp * 8));
-    HIPCHK(hipMemsetAsync(ctx->Lm.p, 0, (size_t)mp * mp * 8, s));
-    HIPCHK(hipMemsetAsync(ctx->Lb.p, 0, (size_t)mp * mp * 8, s));
-    ctx->lm_zeroed = (size_t)mp;
+    HIPCHK(zero_factor(ctx, ctx->Lm.d(), mp, s));
+    HIPCHK(zero_factor(ctx, ctx->Lb.d(), mp, s));
   }
   HIPCHK(ensure(ctx, ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(mp) * 8)));
   HIPCHK(ensure(ctx, ctx->ldm, mp * 8));
@@ -3184,6 +3207,25 @@ int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
   ctx->lgroup = G;
   ctx->nranks = nranks;
   ctx->rank = rank;
+  return 0;
+}
+
+int gps_comm_info(gps_ctx* ctx, int* nranks, int* rank, int* kind) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(nranks && rank && kind, "out pointer is NULL");
+  if (ctx->comm) {  // what the RCCL communicator itself holds, not what the caller asked for
+    NCCLCHK(ncclCommCount(ctx->comm, nranks));
+    NCCLCHK(ncclCommUserRank(ctx->comm, rank));
+    *kind = GPS_COMM_RCCL;
+  } else if (ctx->lgroup) {
+    *nranks = ctx->lgroup->n;
+    *rank = ctx->rank;
+    *kind = GPS_COMM_LOCAL;
+  } else {
+    *nranks = 1;
+    *rank = 0;
+    *kind = GPS_COMM_NONE;
+  }
   return 0;
 }
 

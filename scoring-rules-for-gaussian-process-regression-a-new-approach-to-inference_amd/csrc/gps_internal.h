@@ -89,7 +89,6 @@ GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 extern int g_stream_k;   // 1: the stream-K tail of uniform-K 128-tile launches (launch_gemm)
-extern int g_gemm_glds;  // 1: 128-tile launches stage operands global -> LDS directly (glds)
 extern int g_gemm_prio;  // s_setprio around the mainloop's MFMA phase: 0 off, 1 (default) products, 2 all
 extern int g_slab_xcd;   // split-K launches: each XCD runs whole K slices (GPS_OPT_SLAB_XCD)
 constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)
@@ -263,10 +262,9 @@ struct DagParams {
   unsigned long long spin_ticks;   // 100 MHz s_memrealtime ticks a dependency wait may take
   unsigned long long* trace = nullptr;  // diagnostics only (tools/dag_bench.cpp): 4 words per slot
   int group = 3;                   // 16-deep operand chunks per load group of a strip task (2..4)
-  int split = 0;                   // the task list is a split-chain one (dag_task_list split)
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
-std::vector<uint32_t> dag_task_list(int T, int order = 1, bool fine = true, bool split = false);
+std::vector<uint32_t> dag_task_list(int T, int order = 1, bool fine = true);
 inline int64_t dag_cnt_ints(int T) { return (16 + 2 * (int64_t)T * T + 63) / 64 * 64; }
 
 // y[i] = sum_k L[i][k] x[k] over the tile-lower part (rows < n_pad)

@@ -87,21 +87,6 @@ __device__ __forceinline__ bool tile_of(const GemmParams& p, int t, int& ti, int
     tj = p.tri == TRI_K_LE_J ? p.tiles_n - 1 - cj : cj;
     return ti < p.tiles_m && cj < p.tiles_n;
   }
-  if (p.map_mode == 7) {
-    // XCD-banded, band index inner (A/B): as map 3, XCD x owns a contiguous band of the index
-    // that does not carry the triangular work, but walks it panel by panel: the tiles of one
-    // band panel (every value of the work index, heaviest first) are consecutive, so they are
-    // co-resident and read that panel once from HBM into the XCD's L2
-    const int x = t & 7, i = t >> 3;
-    const bool wi = p.tri == TRI_K_LE_I || p.tri == TRI_K_GE_I;
-    const int nb = wi ? p.tiles_n : p.tiles_m, nw = wi ? p.tiles_m : p.tiles_n;
-    const int bb = (nb + 7) >> 3, bi = x * bb + i / nw, wk = i % nw;
-    if (bi >= nb || i / nw >= bb) return false;
-    const int widx = (p.tri == TRI_K_LE_I || p.tri == TRI_K_LE_J) ? nw - 1 - wk : wk;
-    ti = wi ? widx : bi;
-    tj = wi ? bi : widx;
-    return true;
-  }
   if (p.map_mode == 5) {
     // XCD-banded 8×8 patches (the automatic order of the FITC row norms): as map 3, XCD x owns
     // a band of the index that does not carry the triangular work, but its resident tiles form 8 (band) × 8
@@ -140,14 +125,14 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <int ALAY, int BLAY, int EPI, int TILE, bool GL = false>
+template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o = -1, int ke_o = -1,
                                           double* part = nullptr);
 template <int ALAY, int BLAY>
 __device__ void gemm_sk_block(const GemmParams& p, int s, double* smem);
 
-template <int ALAY, int BLAY, int EPI, int TILE, bool GL>
+template <int ALAY, int BLAY, int EPI, int TILE>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
   constexpr int STAGE = 2 * BK * LS;     // one buffer: A image + B image
@@ -168,12 +153,12 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     const int nt = (int)gridDim.x;
     const int l = xcd_remap((int)(blockIdx.x + blockIdx.y * gridDim.x), nt * (int)gridDim.y);
     if (!tile_of(p, l % nt, ti, tj)) return;
-    gemm_tile<ALAY, BLAY, EPI, TILE, GL>(p, ti, tj, l / nt, smem);
+    gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, l / nt, smem);
     return;
   }
   const int nblk = p.sk_wgs > 0 ? p.sk_dp : (int)gridDim.x;
   if (!tile_of(p, remap ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x, ti, tj)) return;
-  gemm_tile<ALAY, BLAY, EPI, TILE, GL>(p, ti, tj, blockIdx.y, smem);
+  gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, blockIdx.y, smem);
 }
 
 // EPI_STORE epilogue: C = alpha·acc (+ beta·C) for this thread's accumulators
@@ -280,7 +265,7 @@ __device__ void gemm_sk_block(const GemmParams& p, int s, double* smem) {
   }
 }
 
-template <int ALAY, int BLAY, int EPI, int TILE, bool GL>
+template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o, int ke_o, double* part) {
   constexpr int LS = TILE + 16;          // LDS row stride (doubles)
@@ -436,78 +421,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     }
   };
 
-  if constexpr (GL) {
-    // ---- direct global -> LDS staging (GPS_OPT_GEMM_GLDS): global_load_lds_dwordx4, no
-    // staging registers and no ds_write pass.  One wave instruction lands 1 KB contiguously
-    // (lane l at base + 16 l), so i-major sources ([i][k]: A with LAY_N, B with LAY_T) get an
-    // unpadded i-major image — 16-double rows, 16-byte chunk c of row r stored at chunk
-    // c ^ ((r >> 1) & 7) (the permutation goes on the SOURCE address, cdna_hip_programming.md
-    // rule 21), which makes the fragment reads (16 rows, one k) conflict-free — and k-major
-    // sources keep the padded k-major image (each wave instruction is exactly one 1-KB k row).
-    // Fragments take the same k order as the register path: bitwise the same products.
-    typedef __attribute__((address_space(3))) void* lds_ptr_t;
-    typedef __attribute__((address_space(1))) void* gbl_ptr_t;
-    auto glds_imaj = [&](const double* src, int64_t ld, int base, int k0, double* img) {
-#pragma unroll
-      for (int q = 0; q < TILE / 32; ++q) {  // rows 32·wave + 8q .. +8, one instruction each
-        const int r0 = (TILE / 4) * wave + 8 * q, r = r0 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (int64_t)(base + r) * ld + k0 + 2 * c),
-                                         (lds_ptr_t)(img + r0 * BK), 16, 0, 0);
-      }
-    };
-    auto glds_kmaj = [&](const double* src, int64_t ld, int base, int k0, double* img) {
-#pragma unroll
-      for (int q = 0; q < BK / 4; ++q) {  // k rows 4·wave + q (TILE = 128: one instruction each)
-        const int k = (BK / 4) * wave + q;
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + (int64_t)(k0 + k) * ld + base + 2 * lane),
-                                         (lds_ptr_t)(img + k * LS), 16, 0, 0);
-      }
-    };
-    auto stage = [&](int buf, int k0) {
-      double* As = smem + buf * STAGE;
-      double* Bs = As + BK * LS;
-      if constexpr (ALAY == LAY_N) glds_imaj(p.A, p.lda, row0, k0, As);
-      else glds_kmaj(p.A, p.lda, row0, k0, As);
-      if constexpr (BLAY == LAY_T) glds_imaj(p.B, p.ldb, col0, k0, Bs);
-      else glds_kmaj(p.B, p.ldb, col0, k0, Bs);
-    };
-    auto frag = [&](const double* img, bool imaj, int r, int k) {
-      return imaj ? img[r * BK + 2 * ((k >> 1) ^ ((r >> 1) & 7)) + (k & 1)] : img[k * LS + r];
-    };
-    auto compute_gl = [&](int buf) {
-      const double* As = smem + buf * STAGE;
-      const double* Bs = As + BK * LS;
-#pragma unroll
-      for (int kk = 0; kk < BK / 4; ++kk) {
-        const int k = kk * 4 + (lane >> 4);
-        double a[MI], b[MI];
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) a[mi] = frag(As, ALAY == LAY_N, wr * WT + mi * 16 + (lane & 15), k);
-#pragma unroll
-        for (int ni = 0; ni < MI; ++ni) b[ni] = frag(Bs, BLAY == LAY_T, wc * WT + ni * 16 + (lane & 15), k);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < MI; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-      }
-    };
-    if (nk > 0) {
-      stage(0, kb);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      // steady state: slice it+1's loads go out before slice it is multiplied; each wave waits
-      // for its own DMA, then the barrier publishes every wave's (MI355X_MICROARCH item 7)
-      for (int it = 0; it < nk - 1; ++it) {
-        stage((it + 1) & 1, kb + (it + 1) * BK);
-        compute_gl(it & 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-      compute_gl((nk - 1) & 1);
-    }
-  } else if (nk > 0) {
+  if (nk > 0) {
     load_tile(kb);
     store_tile(0);
     __syncthreads();
@@ -813,7 +727,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_sym_kernel(const double* __
 }
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
-int g_gemm_glds = 0;  // GPS_OPT_GEMM_GLDS (process-wide): direct-to-LDS staging of 128-tiles
 int g_gemm_prio = 1;  // GPS_OPT_GEMM_PRIO (process-wide): s_setprio around the MFMA phase
 // GPS_OPT_SLAB_XCD (process-wide): split-K launches slice-major per XCD.  The FITC SYRK's L2-fabric
 // bytes 4.48 -> 1.91 GB per C4 launch (7x -> 2.9x its Knm operand), time neutral (C4 11.86 -> 11.83,
@@ -909,6 +822,9 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // alpha/beta; without one (legacy FITC path) slice s writes C + s*c_kslice_stride
   const bool slabbed = p.ksplit > 1 && p.ws != nullptr;
   if (p.ksplit > 1 && !slabbed && (epi != EPI_STORE || p.beta != 0.0)) return hipErrorInvalidValue;
+  // a symmetric result is mirrored from the one reduced C; unslabbed slices land in separate
+  // C + s·c_kslice_stride blocks, so there is nothing whole to mirror
+  if (p.ksplit > 1 && !slabbed && p.mirror) return hipErrorInvalidValue;
   GemmParams q = p;
   if (slabbed) {
     if (epi != EPI_STORE) return hipErrorInvalidValue;
@@ -925,24 +841,16 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build; the
   // FITC row norms (EPI_ROWSQ) to its 8×8-patch form (map 5): C5 174.0 vs 181.5 ms, while the
   // patch order on the factorisation / predictive TRMMs cost C3 27 % (profiles/r2_map5_ab.txt)
-  // 6 / 8: the automatic order with map 3 / 7 for the row norms (A/B runs; both slower in the
-  // library on C4 or C5: profiles/r4_rowsq_map_ab.txt)
-  const int rowsq_map = q.map_mode == 6 ? 3 : q.map_mode == 8 ? 7 : 5;
-  if (q.map_mode == 6 || q.map_mode == 8) q.map_mode = 0;
+  // (the row norms in map 3 or in panel-inner bands measured slower in the library on C4 or C5:
+  // profiles/r4_rowsq_map_ab.txt)
   if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out)
-    q.map_mode = (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) ? rowsq_map : 3;
+    q.map_mode = (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) ? 5 : 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
   if (q.map_mode == 5 && (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J)) q.map_mode = 0;
   if (q.map_mode == 5) {  // 8 XCDs × ceil(work / 8) groups × the band's 8-wide groups × 64
     const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;
     const int nb = wi ? q.tiles_n : q.tiles_m, nw = wi ? q.tiles_m : q.tiles_n;
     tiles = 8 * ((nw + 7) / 8) * (((nb + 7) / 8 + 7) / 8) * 64;
-  }
-  if (q.map_mode == 7) {
-    if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
-    const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;
-    const int nb = wi ? q.tiles_n : q.tiles_m, nw = wi ? q.tiles_m : q.tiles_n;
-    tiles = 8 * ((nb + 7) / 8) * nw;
   }
   if (q.map_mode == 3) {
     if (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J) return hipErrorInvalidValue;
@@ -971,16 +879,10 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
                (q.map_mode == 0 || q.map_mode == 2) && (q.lower_out || q.tri == TRI_NONE);
   dim3 grid(tiles, q.ksplit), block(256);
   hipError_t err = hipErrorInvalidValue;
-  // direct-to-LDS staging (GPS_OPT_GEMM_GLDS): 128-tiles without a per-k operand scale, the
-  // stream-K tail, or the row-dot epilogue (which reads the k-major A image)
-  const bool gl = g_gemm_glds && tile == 128 && !q.kscale && q.sk_wgs == 0 && epi != EPI_ROWSQ_DOT;
-#define GPS_GEMM_CASE(AL, BL, EP, T)                                                          \
-  if (err == hipErrorInvalidValue && alay == AL && blay == BL && epi == EP && tile == T) {   \
-    if (T == 128 && gl)                                                                       \
-      hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T, (T == 128)>), grid, block, 0, s, q); \
-    else                                                                                      \
-      hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T, false>), grid, block, 0, s, q);    \
-    err = hipGetLastError();                                                                  \
+#define GPS_GEMM_CASE(AL, BL, EP, T)                                                        \
+  if (err == hipErrorInvalidValue && alay == AL && blay == BL && epi == EP && tile == T) { \
+    hipLaunchKernelGGL((gemm_f64_kernel<AL, BL, EP, T>), grid, block, 0, s, q);            \
+    err = hipGetLastError();                                                                \
   }
   GPS_GEMM_CASE(LAY_N, LAY_T, EPI_STORE, 128)
   GPS_GEMM_CASE(LAY_N, LAY_N, EPI_STORE, 128)

@@ -294,12 +294,7 @@ __device__ __forceinline__ int tail_k(int wave, int slot) {
 // The leaf as a device function of one 256-thread workgroup: the stand-alone kernel below
 // (COH = false) and the persistent factorisation's LEAF task (COH = true: A read and L⁻¹ written
 // coherently, since other workgroups of the same launch produce / consume them).  S, DG: LDS.
-// INV = false (the persistent factorisation's split chain, GPS_OPT_DAG_SPLIT): L only — every
-// panel also goes write-through into A's diagonal tile (in place: the leaf has A in LDS), the 8
-// diagonal 16×16 inverses X_pp into L⁻¹ as before, and the rest of X = L⁻¹ (the T_k products,
-// the X finish, the tail: 10 of the leaf's 36 µs, profiles/r4_leaf_probe_skip.txt) is left to an
-// INV task off the chain (inv_body below).
-template <bool COH, bool INV = true>
+template <bool COH>
 __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t lda,
                                           double* __restrict__ Linv, int64_t ldl,
                                           double* __restrict__ Lout, int64_t ldlo,
@@ -359,13 +354,6 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
 #pragma unroll
           for (int c = 0; c < 8; ++c) dst[c] = (dv2){P[s][2 * c], P[s][2 * c + 1]};
         }
-        if constexpr (!INV) {
-          if (R >= t0) {
-            double* dst = const_cast<double*>(A) + (int64_t)R * lda + t0;
-#pragma unroll
-            for (int c = 0; c < 16; ++c) st_d<COH>(dst + c, P[s][c]);
-          }
-        }
       }
     } else if (p >= 1) {
       const int pp = p - 1;
@@ -379,12 +367,10 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
         invert_diag<COH>(S, DG, pp, lane, Linv, ldl);
         if (lane < 16) logdiag[16 * pp + lane] = log(DG[16 * pp + lane]);
       }
-      if constexpr (INV) {
 #pragma unroll
-        for (int slot = 0; slot < 3; ++slot) {
-          const int k = uw + 3 * slot;
-          if (k < pp) T[slot] = inv_row_t(S, pp, k, lane);
-        }
+      for (int slot = 0; slot < 3; ++slot) {
+        const int k = uw + 3 * slot;
+        if (k < pp) T[slot] = inv_row_t(S, pp, k, lane);
       }
     }
     __syncthreads();
@@ -397,7 +383,7 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
     } else if (wave == 0) {
       invert_diag<COH>(S, DG, 7, lane, Linv, ldl);
     }
-    if (INV && p >= 1 && wave != 0) {
+    if (p >= 1 && wave != 0) {
       const int pp = p - 1, td = tix(pp, pp);
 #pragma unroll
       for (int slot = 0; slot < 3; ++slot) {
@@ -419,15 +405,13 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
     __syncthreads();
   }
   // ================= tail: X row 7 (T_k on all 4 waves, 7 tile products each), then finish
-  if constexpr (INV) {
 #pragma unroll
-    for (int slot = 0; slot < 2; ++slot) {
-      const int k = tail_k(wave, slot);
-      if (k >= 0) T[slot] = inv_row_t(S, 7, k, lane);
-    }
+  for (int slot = 0; slot < 2; ++slot) {
+    const int k = tail_k(wave, slot);
+    if (k >= 0) T[slot] = inv_row_t(S, 7, k, lane);
   }
   __syncthreads();  // (X row 6 and X_77 were final before; only the reads above precede this)
-  if constexpr (INV) {
+  {
     const int td = tix(7, 7);
 #pragma unroll
     for (int slot = 0; slot < 2; ++slot) {
@@ -455,126 +439,6 @@ __device__ __forceinline__ void leaf_body(const double* __restrict__ A, int64_t 
   // panel, are not written: every caller zeroes the factor buffers when it (re)allocates them and
   // nothing writes there afterwards — round 4: 57 KB less write-through traffic to drain at the
   // end of every persistent LEAF)
-}
-
-// L_kk's lower tiles into LDS for the split chain's INV and TRSM' tasks: the 28 tiles below the
-// tile diagonal from L (written through by LEAF' into A's diagonal tile), the 8 diagonal tiles
-// from L⁻¹ (X_pp, written by LEAF''s invert_diag) — the layout the leaf's inverse steps read.
-template <bool COH>
-__device__ __forceinline__ void load_l_xdiag(const double* L, int64_t lda, const double* X,
-                                             int64_t ldl, double* S) {
-  const int tid = threadIdx.x;
-  const int hb = tid >> 7, q = tid & 127, r = q >> 3, c2 = (q & 7) * 2;
-  dv2 v[18];
-#pragma unroll
-  for (int m = 0; m < 18; ++m) {
-    const int t = 2 * m + hb;
-    const int ti = tile_i(t), tj = t - tix(ti, 0);
-    v[m] = ti == tj ? ld_d2<COH>(X + (int64_t)(16 * ti + r) * ldl + 16 * tj + c2)
-                    : ld_d2<COH>(L + (int64_t)(16 * ti + r) * lda + 16 * tj + c2);
-  }
-#pragma unroll
-  for (int m = 0; m < 18; ++m) {
-    const int t = 2 * m + hb;
-    S[t * TSZ + r * TS + c2] = v[m].x;
-    S[t * TSZ + r * TS + c2 + 1] = v[m].y;
-  }
-}
-
-// INV(k) of the split chain: X_kk = L_kk⁻¹ from L_kk and its diagonal inverses X_pp, by block
-// rows r = 1..7 (X_rk = −X_rr Σ_{j=k}^{r−1} L_rj X_jk, the leaf's inverse step without the
-// factorisation around it); row r's T_k go to wave w as the pair k = w, r − 1 − w (r + 1 tile
-// products each).  Off the chain: X_kk feeds the trailing TRSMs and the inverse tasks only.
-template <bool COH>
-__device__ __forceinline__ void inv_body(const double* L, int64_t lda, double* Linv, int64_t ldl,
-                                         double* S) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  load_l_xdiag<COH>(L, lda, Linv, ldl, S);
-  __syncthreads();
-#pragma unroll 1
-  for (int r = 1; r < 8; ++r) {
-    const int ka = wave, kb = r - 1 - wave;
-    d4 Ta, Tb;
-    if (ka <= kb) Ta = inv_row_t(S, r, ka, lane);
-    if (ka < kb) Tb = inv_row_t(S, r, kb, lane);
-    __syncthreads();  // every read of L row r precedes the X_rk overwriting it
-    const int td = tix(r, r);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = u ? kb : ka;
-      if (u ? ka < kb : ka <= kb) {
-        const d4 T = u ? Tb : Ta;
-        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) acc = mfma(-opnd(S, td, lane, kk), T[kk], acc);
-        const int tdst = tix(r, k);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          S[acc_off(tdst, lane, q)] = acc[q];
-          st_d<COH>(Linv + (int64_t)(16 * r + 4 * q + (lane >> 4)) * ldl + 16 * k + (lane & 15), acc[q]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// TRSM'(k+1, k) of the split chain, one workgroup: 64 rows of L_{k+1,k} = A_{k+1,k} L_kk⁻ᵀ by
-// blocked forward substitution over the 8 column panels, with L_kk and X_pp in S (load_l_xdiag)
-// and the 64 rows in SA (row stride TSA), 16 per wave:
-//   Y_p = A[:, p] − Σ_{q<p} L[:, q] L_kk[p, q]ᵀ,   L[:, p] = Y_p X_ppᵀ,
-// carried transposed (Y_pᵀ = A[:, p]ᵀ − L_kk[p, q] · L[:, q]ᵀ, L[:, p]ᵀ = X_pp Y_pᵀ: the f64
-// MFMA's C/D map puts row (l >> 4) + 4e, column l & 15 in lane l, which is the B-operand map),
-// each finished panel written back over its A panel in SA, where the later panels read it.
-constexpr int TSA = 132;  // SA row stride (doubles): the transposed reads fall on distinct banks
-template <bool COH>
-__device__ __forceinline__ void trsm_sub_load(const double* C, int64_t ldc, double* SA) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {  // 64 rows × 64 pairs, 16 pairs per thread
-    const int e = tid + 256 * m, r = e >> 6, c2 = (e & 63) * 2;
-    const dv2 v = ld_d2<COH>(C + (int64_t)r * ldc + c2);
-    SA[r * TSA + c2] = v.x;
-    SA[r * TSA + c2 + 1] = v.y;
-  }
-}
-__device__ __forceinline__ void trsm_sub_wave(const double* S, double* SA) {
-  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  double* row = SA + (int64_t)(16 * ((int)threadIdx.x >> 6) + r) * TSA;
-  // (runtime loops: unrolled, the 8×8 triangle's operand reads were hoisted into registers and the
-  //  kernel spilled)
-#pragma unroll 1
-  for (int p = 0; p < 8; ++p) {
-    d4 acc;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc[e] = row[16 * p + g + 4 * e];
-#pragma unroll 1
-    for (int q = 0; q < p; ++q) {
-      double b[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) b[kk] = row[16 * q + 4 * kk + g];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) acc = mfma(-opnd(S, tix(p, q), lane, kk), b[kk], acc);
-    }
-    d4 y = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) y = mfma(opnd(S, tix(p, p), lane, kk), acc[kk], y);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) row[16 * p + g + 4 * e] = y[e];
-  }
-}
-template <bool COH>
-__device__ __forceinline__ void trsm_sub_store(const double* SA, double* C, int64_t ldc, double* C2,
-                                               int64_t ldc2) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const int e = tid + 256 * m, r = e >> 6, c2 = (e & 63) * 2;
-    const dv2 v = (dv2){SA[r * TSA + c2], SA[r * TSA + c2 + 1]};
-    st_d2<COH>(C + (int64_t)r * ldc + c2, v);
-    if (C2) *reinterpret_cast<dv2*>(C2 + (int64_t)r * ldc2 + c2) = v;
-  }
 }
 
 __global__ __launch_bounds__(256) void potrf_leaf_v4_kernel(
@@ -854,15 +718,9 @@ __device__ __forceinline__ void run_fine(const Fine& s) {
 #ifndef GPS_DAG_WAVES_PER_EU
 #define GPS_DAG_WAVES_PER_EU 1
 #endif
-// SPLIT: the split chain's task types (5-7) compiled in — a separate instantiation, because their
-// code raises the kernel's register allocation into scratch spills on every path (the default
-// instantiation keeps 0 spills)
-template <bool TRACE, int G, bool SPLIT = false>
+template <bool TRACE, int G>
 __global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(DagParams p) {
   __shared__ double S[v4::NT * v4::TSZ];
-  // TRSM' row strips (the split chain): 64 × 132 doubles, 66 KB more LDS (145 KB in all; one
-  // workgroup per CU either way — the leaf's registers already take the whole CU)
-  __shared__ __attribute__((aligned(16))) double SA[SPLIT ? 64 * v4::TSA : 2];
   __shared__ double DG[128];
   __shared__ unsigned int sh[3];  // [task word, abort, queue slot]
   const int tid = threadIdx.x;
@@ -919,19 +777,9 @@ __global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(Da
         case 0:  // LEAF(k = ti)
           c0 = acnt + ti * T + ti; v0 = U * ti;
           break;
-        case 1:  // TRSM(i, k): A_ik final, X_kk (LEAF or, split, INV)
+        case 1:  // TRSM(i, k): A_ik final, X_kk from LEAF(k)
           c0 = acnt + ti * T + tk; v0 = U * tk;
           c1 = xcnt + tk * T + tk; v1 = 1;
-          break;
-        case 5:  // LEAF'(k), split chain
-          c0 = acnt + ti * T + ti; v0 = U * ti;
-          break;
-        case 6:  // INV(k): L_kk and X_pp from LEAF'(k)
-          c0 = acnt + ti * T + ti; v0 = U * ti + 1;
-          break;
-        case 7:  // TRSM'(k+1, k): A_{k+1,k} final, L_kk and X_pp from LEAF'(k)
-          c0 = acnt + ti * T + tk; v0 = U * tk;
-          c1 = acnt + tk * T + tk; v1 = U * tk + 1;
           break;
         case 2:  // UPD(i, j, k)
           c0 = acnt + ti * T + tk; v0 = U * (tk + 1);
@@ -997,29 +845,6 @@ __global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(Da
       out = acnt + ti * T + ti;
       out2 = xcnt + ti * T + ti;
       inc = 1;
-    } else if (SPLIT && type == 5) {  // LEAF'(k): L_kk (into A's diagonal tile too) and the X_pp only
-      const int64_t o = (int64_t)128 * ti;
-      v4::leaf_body<true, false>(p.A + o * lda + o, lda, p.Linv + o * ldl + o, ldl,
-                                 p.Lout ? p.Lout + o * p.ldlo + o : nullptr, p.ldlo, p.logdiag + o,
-                                 p.info, p.base + (int)o, p.nreal - (int)o, S, DG);
-      out = acnt + ti * T + ti;
-      inc = 1;
-    } else if (SPLIT && type == 6) {  // INV(k): X_kk
-      const int64_t o = (int64_t)128 * ti;
-      v4::inv_body<true>(p.A + o * lda + o, lda, p.Linv + o * ldl + o, ldl, S);
-      out = xcnt + ti * T + ti;
-      inc = 1;
-    } else if (SPLIT && type == 7) {  // TRSM'(k+1, k): rows 64·part.., blocked substitution
-      const int64_t K = 128 * (int64_t)tk, R = 128 * (int64_t)ti + 64 * part;
-      v4::load_l_xdiag<true>(p.A + K * lda + K, lda, p.Linv + K * ldl + K, ldl, S);
-      v4::trsm_sub_load<true>(p.A + R * lda + K, lda, SA);
-      __syncthreads();
-      v4::trsm_sub_wave(S, SA);
-      __syncthreads();
-      v4::trsm_sub_store<true>(SA, p.A + R * lda + K, lda, p.Lout ? p.Lout + R * p.ldlo + K : nullptr,
-                               p.ldlo);
-      out = acnt + ti * T + tk;
-      inc = U / 2;
     } else if (fine) {
       Fine f;
       const int64_t R = 128 * (int64_t)ti, K = 128 * (int64_t)tk;
@@ -1141,9 +966,7 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
     return hipErrorInvalidValue;
   // every strip's buffer descriptor spans at most 128 rows of its matrix (32-bit offsets)
   if ((int64_t)128 * std::max(p.lda, p.ldl) * 8 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-  if (p.split && p.group != 3) return hipErrorInvalidValue;
-  auto k = p.split ? (p.trace ? dag::potrf_dag_kernel<true, 3, true> : dag::potrf_dag_kernel<false, 3, true>)
-         : p.trace ? (p.group == 2 ? dag::potrf_dag_kernel<true, 2>
+  auto k = p.trace ? (p.group == 2 ? dag::potrf_dag_kernel<true, 2>
                                     : p.group == 3 ? dag::potrf_dag_kernel<true, 3> : dag::potrf_dag_kernel<true, 4>)
                    : (p.group == 2 ? dag::potrf_dag_kernel<false, 2>
                                     : p.group == 3 ? dag::potrf_dag_kernel<false, 3> : dag::potrf_dag_kernel<false, 4>);
@@ -1163,15 +986,15 @@ hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s) {
 //            it), with the durations the round-4 traces measured (below);
 //   order 2: the same with round 3's weights (leaf 38, strip 9, fine part 4, hand-off 1).
 // fine: the leaf chain's TRSM(k+1,k) and UPD(k+1,k+1,k) as fine parts (8 / 16, see run_fine).
-// split: the chain without the leaf's inverse — LEAF'(k) (type 5: L_kk and the X_pp), INV(k)
-// (type 6: X_kk, off the chain), TRSM'(k+1,k) (type 7, 2 parts: substitution with L_kk and the
-// X_pp); the other TRSM(i,k) and the inverse tasks take X_kk from INV(k).
+// (Round 4's split chain — the leaf without its inverse, TRSM(k+1,k) by substitution, an INV task
+// off the chain — measured slower and was removed: profiles/r4_dag_split_ab.txt,
+// profiles/r5_prune_split_chain.diff.)
 // Word: type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24.
 // order 1's weights, µs: LEAF, fine part, TRSM, UPD, UPDX, FIN strips, hand-off (tools/dag_bench
 // overrides them for sweeps; the library never writes them)
 double g_dag_weights[7] = {35.0, 6.0, 9.7, 11.7, 11.2, 9.3, 2.5};
 
-std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
+std::vector<uint32_t> dag_task_list(int T, int order, bool fine) {
   struct Task { int type, i, j, k; std::vector<int> deps; double est = 0.0, rank = 0.0; };
   auto is_fine = [&](const Task& t) {
     return fine && ((t.type == 1 && t.i == t.k + 1) || (t.type == 2 && t.i == t.k + 1 && t.j == t.i));
@@ -1189,11 +1012,9 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
   };
   // factorisation, right-looking (generation order is topological)
   for (int k = 0; k < T; ++k) {
-    leaf[k] = add(split ? 5 : 0, k, k, k, {upd_last[k * T + k]});
-    xkk[k] = split ? add(6, k, k, k, {leaf[k]}) : leaf[k];  // the task X_kk comes from
-    for (int i = k + 1; i < T; ++i)
-      trsm[i * T + k] = split && i == k + 1 ? add(7, i, k, k, {upd_last[i * T + k], leaf[k]})
-                                            : add(1, i, k, k, {upd_last[i * T + k], xkk[k]});
+    leaf[k] = add(0, k, k, k, {upd_last[k * T + k]});
+    xkk[k] = leaf[k];  // the task X_kk comes from
+    for (int i = k + 1; i < T; ++i) trsm[i * T + k] = add(1, i, k, k, {upd_last[i * T + k], xkk[k]});
     for (int j = k + 1; j < T; ++j)
       for (int i = j; i < T; ++i)
         upd_last[i * T + j] = add(2, i, j, k, {trsm[i * T + k], trsm[j * T + k], upd_last[i * T + j]});
@@ -1213,12 +1034,12 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
   for (int t = 0; t < n; ++t)
     for (int d : tk[t].deps) { succ[d].push_back(t); ++indeg[t]; }
   if (order == 0) {
-    auto dur = [&](const Task& t) { return t.type == 0 || t.type == 5 ? 36.0 : 4.0; };
+    auto dur = [&](const Task& t) { return t.type == 0 ? 36.0 : 4.0; };
     for (int t = 0; t < n; ++t)  // generation order is topological
       for (int d : tk[t].deps) tk[t].est = std::max(tk[t].est, tk[d].est + dur(tk[d]) + 3.0);
   } else if (order == 2) {  // round 3's weights
     auto dur = [&](const Task& t) {
-      return t.type == 0 ? 38.0 : t.type == 5 ? 27.0 : t.type == 6 ? 10.0 : is_fine(t) ? 4.0 : 9.0;
+      return t.type == 0 ? 38.0 : is_fine(t) ? 4.0 : 9.0;
     };
     for (int t = n - 1; t >= 0; --t) {
       double m = 0.0;
@@ -1238,10 +1059,7 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
         case 1: return w[2];
         case 2: return w[3];
         case 3: return w[4];
-        case 4: return w[5];
-        case 5: return 39.0;
-        case 6: return 14.0;
-        default: return 21.0;
+        default: return w[5];
       }
     };
     for (int t = n - 1; t >= 0; --t) {  // reverse generation order: successors first
@@ -1261,8 +1079,7 @@ std::vector<uint32_t> dag_task_list(int T, int order, bool fine, bool split) {
     ready.pop();
     const Task& x = tk[t];
     const bool f = is_fine(x);
-    const int parts = x.type == 0 || x.type == 5 || x.type == 6 ? 1 : x.type == 7 ? 2
-                      : !f ? dag::NP : x.type == 1 ? dag::NPF_TRSM : dag::NPF_UPD;
+    const int parts = x.type == 0 ? 1 : !f ? dag::NP : x.type == 1 ? dag::NPF_TRSM : dag::NPF_UPD;
     for (int q = 0; q < parts; ++q)
       out.push_back((uint32_t)x.type | (uint32_t)q << 3 | (uint32_t)f << 7 | (uint32_t)x.i << 8 |
                     (uint32_t)x.j << 16 | (uint32_t)x.k << 24);

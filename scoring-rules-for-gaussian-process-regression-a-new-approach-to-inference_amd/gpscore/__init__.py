@@ -8,8 +8,8 @@ Drop-in layers:
   * ``gpscore.dist``    — one process per GPU, FITC row sharding;
   * ``gpscore._lib``    — the ctypes binding of libgpscore.so (include/gpscore.h).
 """
-from ._lib import (Context, GpsError, NotPositiveDefinite, default_context, load,  # noqa: F401
-                   OBJ_NAMES, SCORE_NAMES)
+from ._lib import (Context, GpsError, NotPositiveDefinite, build_id, check_build_id,  # noqa: F401
+                   default_context, load, OBJ_NAMES, SCORE_NAMES)
 from .gp import GP, FitResult, fit, pack_theta, score, surface  # noqa: F401
 
 __version__ = "0.1.0"

@@ -14,6 +14,10 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
+ABI_VERSION = 500  # include/gpscore.h GPS_ABI_VERSION: the signatures below are this version's
+GPS_N_STATS = 6
+GPS_COMM_NONE, GPS_COMM_RCCL, GPS_COMM_LOCAL = 0, 1, 2
+COMM_KINDS = {GPS_COMM_NONE: "none", GPS_COMM_RCCL: "rccl", GPS_COMM_LOCAL: "local"}
 
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
@@ -25,9 +29,7 @@ GPS_OPT_DAG_TILES = 13
 GPS_OPT_DAG_GROUP = 17
 GPS_OPT_STREAM_K = 18
 GPS_OPT_DAG_WGS = 19
-GPS_OPT_GEMM_GLDS = 21
 GPS_OPT_DAG_FINE = 22
-GPS_OPT_DAG_SPLIT = 23
 GPS_OPT_GEMM_PRIO = 24
 GPS_OPT_DAG_ORDER = 25
 GPS_OPT_SLAB_XCD = 26
@@ -45,6 +47,7 @@ _P = ctypes.POINTER(ctypes.c_double)
 # name -> (restype, argtypes); every symbol include/gpscore.h declares
 SIGNATURES = {
     "gps_version": (_c_int, []),
+    "gps_build_id": (_c_int, [_c_cp, _c_int]),
     "gps_ctx_create": (_c_int, [_c_int, ctypes.POINTER(_c_vp)]),
     "gps_ctx_destroy": (_c_int, [_c_vp]),
     "gps_last_error": (_c_cp, [_c_vp]),
@@ -52,7 +55,7 @@ SIGNATURES = {
     "gps_ctx_stream": (_c_vp, [_c_vp]),
     "gps_ctx_synchronize": (_c_int, [_c_vp]),
     "gps_ctx_set_option": (_c_int, [_c_vp, _c_int, _c_int]),
-    "gps_ctx_stats": (_c_int, [_c_vp, _c_vp]),
+    "gps_ctx_stats": (_c_int, [_c_vp, _c_vp, _c_int]),
     "gps_dag_task_list": (_c_int, [_c_int, _c_int, _c_vp, _c_int]),
     "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
     "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
@@ -85,6 +88,8 @@ SIGNATURES = {
     "gps_comm_unique_id": (_c_int, [_c_cp]),
     "gps_comm_init": (_c_int, [_c_vp, _c_int, _c_int, _c_cp]),
     "gps_comm_init_local": (_c_int, [_c_vp, _c_int, _c_int, ctypes.c_longlong]),
+    "gps_comm_info": (_c_int, [_c_vp, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
+                               ctypes.POINTER(_c_int)]),
     "gps_comm_destroy": (_c_int, [_c_vp]),
 }
 
@@ -114,12 +119,39 @@ def load():
             f"libgpscore.so not found at {LIB_PATH}: build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C <pkg>/csrc)")
     lib = ctypes.CDLL(LIB_PATH)
+    lib.gps_version.restype = _c_int
+    lib.gps_version.argtypes = []
+    if lib.gps_version() != ABI_VERSION:  # an old library under new signatures would misread
+        raise ImportError(f"{LIB_PATH} has ABI version {lib.gps_version()}, this binding "
+                          f"expects {ABI_VERSION}: rebuild the library")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def build_id():
+    """The source hash the loaded library was built from (gps_build_id)."""
+    lib = load()
+    buf = ctypes.create_string_buffer(80)
+    lib.gps_build_id(buf, len(buf))
+    return buf.value.decode()
+
+
+def check_build_id():
+    """Refuse a library that was not built from the sources checked out beside it: the test
+    suite and smoke() call this, so a passing GPU record names the HEAD sources' build.  Returns
+    the id; when the sources are absent (a deployed library) nothing is compared."""
+    from . import buildid
+    want = buildid.source_hash()
+    got = build_id()
+    if want is not None and got != want:
+        raise ImportError(f"{LIB_PATH} was built from other sources (build id {got[:16]}, the "
+                          f"checked-out csrc/ hashes to {want[:16]}): rebuild it with "
+                          "`make -C <pkg>/csrc`")
+    return got
 
 
 def ptr(a):
@@ -226,11 +258,18 @@ class Context:
     def stats(self):
         """{graphs, graph_cap, graph_overflow, device_bytes, graph_dropped, graph_evicted}
         (gps_ctx_stats)."""
-        import numpy as np
-        out = np.zeros(6, np.int64)
-        self.call("gps_ctx_stats", out.ctypes.data_as(ctypes.c_void_p))
+        out = np.zeros(GPS_N_STATS, np.int64)
+        rc = self.lib.gps_ctx_stats(self.h, out.ctypes.data_as(ctypes.c_void_p), GPS_N_STATS)
+        self.check(0 if rc >= 0 else rc, "gps_ctx_stats")
         return dict(zip(("graphs", "graph_cap", "graph_overflow", "device_bytes", "graph_dropped",
                          "graph_evicted"), (int(v) for v in out)))
+
+    def comm_info(self):
+        """(nranks, rank, kind) of the context's communicator as the library sees it: RCCL's own
+        ncclCommCount / ncclCommUserRank, the in-process group's, or (1, 0, "none")."""
+        n, r, k = _c_int(), _c_int(), _c_int()
+        self.call("gps_comm_info", ctypes.byref(n), ctypes.byref(r), ctypes.byref(k))
+        return n.value, r.value, COMM_KINDS.get(k.value, str(k.value))
 
     def set_stream(self, stream_handle):
         self.call("gps_ctx_set_stream", _c_vp(stream_handle))

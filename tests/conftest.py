@@ -47,6 +47,16 @@ def gpu_ctx():
     return gpscore.Context(0)
 
 
+@pytest.fixture(scope="session", autouse=True)
+def library_is_head_build():
+    """Every session (CPU or GPU) runs against the library built from the checked-out csrc/:
+    gps_build_id must equal the hash of these sources (gpscore/buildid.py), so a passing record
+    names HEAD's build and not a stale or foreign binary."""
+    from gpscore import _lib
+    if os.path.exists(_lib.LIB_PATH):
+        _lib.check_build_id()
+
+
 # ------------------------------------------------------------------ parity floors record
 # Every measured-floor comparison (the BASELINE configs, the shard splits, the CP.R surfaces)
 # records {test: {output: [gpu-vs-reference error, measured floor, absolute cap]}}; the session

@@ -60,3 +60,57 @@ def test_single_gpu_runs_in_process():
     assert r.returncode == 0, r.stderr
     (j,) = _json_lines(r.stdout)
     assert j["n_gpus"] == 1 and j["ranks"][0][:2] == [0, 0]
+
+
+def test_dry_reports_communicator_rank_counts():
+    """The FITC leg's self-check: every rank's communicator count and user rank
+    gathered into fitc.rccl; at --gpus 2 both ranks agree."""
+    r = _run(["--gpus", "2", "--dry"])
+    assert r.returncode == 0, r.stderr
+    (j,) = _json_lines(r.stdout)
+    rc = j["fitc"]["rccl"]
+    assert rc["ranks_seen"] == [2] and rc["all_ranks_agree"], rc
+    assert sorted(p["comm_user_rank"] for p in rc["per_rank"]) == [0, 1]
+    assert "failures" not in j
+
+
+def test_dry_wrong_communicator_count_fails_the_run():
+    """A communicator that counts other than --gpus ranks: the line still prints (it carries the
+    evidence) and the run exits non-zero."""
+    r = _run(["--gpus", "2", "--dry"], {"GPS_BENCH_DRY_COMM_COUNT": "1:1"})
+    assert r.returncode == 4, (r.returncode, r.stderr)
+    (j,) = _json_lines(r.stdout)
+    assert not j["fitc"]["rccl"]["all_ranks_agree"]
+    assert j["fitc"]["rccl"]["ranks_seen"] == [1, 2]
+    assert j["failures"]
+
+
+def test_spawner_forwards_sigterm_to_ranks():
+    """a SIGTERM to the spawner itself (not to its process group) stops the ranks and
+    fails the run instead of orphaning them."""
+    import signal
+    import time
+
+    import psutil
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(MASTER_ADDR="127.0.0.1", GPS_BENCH_DRY_SLEEP="60")
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--dry"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        parent = psutil.Process(p.pid)
+        deadline = time.time() + 60
+        kids = []
+        while time.time() < deadline and len(kids) < 2:
+            kids = parent.children()
+            time.sleep(0.2)
+        assert len(kids) == 2, kids
+        time.sleep(1.0)
+        p.send_signal(signal.SIGTERM)
+        out, err = p.communicate(timeout=45)
+        assert p.returncode == 128 + signal.SIGTERM, (p.returncode, err)
+        gone, alive = psutil.wait_procs(kids, timeout=10)
+        assert not alive, alive
+    finally:
+        if p.poll() is None:
+            p.kill()

@@ -18,12 +18,12 @@ U = 16   # arrivals per finished tile task (dag::U)
 B = 8    # emulated tile edge (the device uses 128; the algebra is edge-independent)
 
 
-def task_list(T, fine=1, split=0, order=1):
+def task_list(T, fine=1, order=1):
     """Queue words decoded as (type, part, i, j, k, fine); order as GPS_OPT_DAG_ORDER."""
     import ctypes
     from gpscore import _lib
     lib = _lib.load()
-    flags = fine | (split << 1) | ({0: 3, 1: 1, 2: 2}[order] << 2)
+    flags = fine | ({0: 3, 1: 1, 2: 2}[order] << 2)
     n = lib.gps_dag_task_list(T, flags, None, 0)
     assert n > 0
     out = (ctypes.c_uint32 * n)()
@@ -35,12 +35,8 @@ def task_list(T, fine=1, split=0, order=1):
 def needs(t, T):
     """(counter array, i, j, threshold) pairs a strip task polls (the kernel's switch)."""
     typ, _, i, j, k, _ = t
-    if typ in (0, 5):
+    if typ == 0:
         return [("a", i, i, U * i)]
-    if typ == 6:
-        return [("a", i, i, U * i + 1)]
-    if typ == 7:
-        return [("a", i, k, U * k), ("a", k, k, U * k + 1)]
     if typ == 1:
         return [("a", i, k, U * k), ("x", k, k, 1)]
     if typ == 2:
@@ -58,7 +54,6 @@ class Emu:
         self.T = T
         self.A = A.copy()
         self.X = np.full_like(A, np.nan)  # stale contents: every tile must be written first
-        self.Lkk = {}  # split chain: L_kk as LEAF' publishes it (the device: A's diagonal tile)
         self.cnt = {"a": np.zeros((T, T), int), "x": np.zeros((T, T), int)}
 
     def ready(self, t):
@@ -71,21 +66,6 @@ class Emu:
         typ, part, i, j, k, fine = t
         if fine:
             return self.run_fine(typ, part, i, j, k)
-        if typ == 5:  # LEAF'(k): L_kk only (the device also writes the 16×16 diagonal inverses)
-            L = np.linalg.cholesky(np.tril(self.blk(self.A, i, i)) + np.tril(self.blk(self.A, i, i), -1).T)
-            self.Lkk[i] = L
-            self.cnt["a"][i, i] += 1
-            return
-        if typ == 6:  # INV(k): X_kk from L_kk
-            self.blk(self.X, i, i)[:] = np.linalg.inv(self.Lkk[i])
-            self.cnt["x"][i, i] += 1
-            return
-        if typ == 7:  # TRSM'(k+1, k): half the rows of L_ik = A_ik L_kk⁻ᵀ by substitution
-            C = self.blk(self.A, i, k)
-            rows = slice(part * B // 2, (part + 1) * B // 2)
-            C[rows] = np.linalg.solve(self.Lkk[k], C[rows].T).T
-            self.cnt["a"][i, k] += U // 2
-            return
         s = B // NP_  # strip width (32 of 128 on the device)
         rows = slice(part * s, (part + 1) * s)
         if typ == 0:  # LEAF(k = i): the leaf reads A_kk's lower triangle
@@ -149,19 +129,17 @@ def check(em, A):
     L = np.tril(em.A, -1) + np.zeros_like(A)
     for t in range(em.T):  # diagonal tiles hold the updated A_kk; L_kk is the leaf's
         blk = slice(t * B, (t + 1) * B)
-        L[blk, blk] = em.Lkk[t] if t in em.Lkk else np.linalg.cholesky(
-            np.tril(em.A[blk, blk]) + np.tril(em.A[blk, blk], -1).T)
+        L[blk, blk] = np.linalg.cholesky(np.tril(em.A[blk, blk]) + np.tril(em.A[blk, blk], -1).T)
     X = np.where(np.tril(np.ones((n, n), bool)), em.X, 0.0)
     assert np.allclose(L, Lr, rtol=1e-12, atol=1e-12)
     assert np.allclose(X, np.linalg.inv(Lr), rtol=1e-11, atol=1e-11)
 
 
 @pytest.mark.parametrize("order", [0, 1, 2])
-@pytest.mark.parametrize("split", [0, 1])
 @pytest.mark.parametrize("fine", [0, 1])
 @pytest.mark.parametrize("T", [2, 3, 5, 8, 13])
-def test_queue_order_is_topological(T, fine, split, order):
-    tl = task_list(T, fine, split, order)
+def test_queue_order_is_topological(T, fine, order):
+    tl = task_list(T, fine, order)
     A = spd(T, T)
     em = Emu(A, T)
     for t in tl:
@@ -169,24 +147,22 @@ def test_queue_order_is_topological(T, fine, split, order):
         em.run(t)
     check(em, A)
     kinds = [t[0] for t in tl]
-    assert kinds.count(5 if split else 0) == T and kinds.count(6) == (T if split else 0)
-    assert kinds.count(7) == (2 * (T - 1) if split else 0)
+    assert kinds.count(0) == T and not set(kinds) - {0, 1, 2, 3, 4}
     nf = sum(t[5] for t in tl if t[0] == 1)
-    assert nf == (NPF[1] * (T - 1) if fine and not split else 0)
-    chain = 0 if split else (T - 1) * (NP_ - NPF[1] if fine else 0)
-    assert kinds.count(1) == NP_ * T * (T - 1) // 2 - chain - (NP_ * (T - 1) if split else 0)
+    assert nf == (NPF[1] * (T - 1) if fine else 0)
+    chain = (T - 1) * (NP_ - NPF[1] if fine else 0)
+    assert kinds.count(1) == NP_ * T * (T - 1) // 2 - chain
     assert kinds.count(4) == NP_ * T * (T - 1) // 2
-    assert all(t[1] < (NPF[t[0]] if t[5] else {0: 1, 5: 1, 6: 1, 7: 2}.get(t[0], NP_)) for t in tl)
+    assert all(t[1] < (NPF[t[0]] if t[5] else {0: 1}.get(t[0], NP_)) for t in tl)
     # the fine parts are exactly the chain's TRSM(k+1,k) and UPD(k+1,k+1,k)
     assert all(t[2] == t[4] + 1 and (t[0] == 1 or t[3] == t[2]) for t in tl if t[5])
 
 
-@pytest.mark.parametrize("split", [0, 1])
 @pytest.mark.parametrize("fine", [0, 1])
 @pytest.mark.parametrize("T,seed", [(4, 0), (6, 1), (9, 2)])
-def test_counters_cover_every_dependency(T, seed, fine, split):
+def test_counters_cover_every_dependency(T, seed, fine):
     """Random execution orders permitted by the thresholds alone (any worker timing)."""
-    tl = task_list(T, fine, split)
+    tl = task_list(T, fine)
     A = spd(T, 10 + seed)
     em = Emu(A, T)
     rng = np.random.default_rng(seed)
@@ -201,10 +177,10 @@ def test_counters_cover_every_dependency(T, seed, fine, split):
 @pytest.mark.parametrize("T", [5, 20])
 def test_orders_queue_the_same_tasks(T):
     """The orders differ only in sequence: same strip multiset, and they do differ."""
-    lists = [task_list(T, 1, 0, o) for o in (0, 1, 2)]
+    lists = [task_list(T, 1, o) for o in (0, 1, 2)]
     assert sorted(lists[0]) == sorted(lists[1]) == sorted(lists[2])
     assert lists[1] != lists[2] and lists[1] != lists[0]
-    assert task_list(T, 1, 0) == lists[1]  # the default
+    assert task_list(T, 1) == lists[1]  # the default
 
 
 def test_queue_sizes():
@@ -217,9 +193,8 @@ def test_queue_sizes():
         n0 = T + NP_ * (T * (T - 1) + upd + updx)
         assert lib.gps_dag_task_list(T, 0, None, 0) == n0
         assert lib.gps_dag_task_list(T, 1, None, 0) == n0 + (T - 1) * (NPF[1] + NPF[2] - 2 * NP_)
-        # split: + T INV tasks, the chain TRSM as 2 substitution parts (fine UPD parts as before)
-        assert lib.gps_dag_task_list(T, 2, None, 0) == n0 + T + (T - 1) * (2 - NP_)
-        assert lib.gps_dag_task_list(T, 3, None, 0) == n0 + T + (T - 1) * (2 - NP_ + NPF[2] - NP_)
+        # bit 1 (round 4's split chain, removed in round 5) and unknown bits are refused
+        assert lib.gps_dag_task_list(T, 2, None, 0) < 0 and lib.gps_dag_task_list(T, 16, None, 0) < 0
     assert lib.gps_dag_task_list(65, 1, None, 0) < 0 and lib.gps_dag_task_list(1, 1, None, 0) < 0
 
 

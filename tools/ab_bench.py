@@ -4,7 +4,7 @@
   python tools/ab_bench.py --config C3 map=0 map=4 ov=0
   options: map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN),
            graph (GPS_OPT_GRAPH), tiny (GPS_OPT_TINY_GEMM),
-           pre (GPS_OPT_PRED_PRE), dag (GPS_OPT_DAG), dagt (GPS_OPT_DAG_TILES), glds (GPS_OPT_GEMM_GLDS), fine (GPS_OPT_DAG_FINE), split (GPS_OPT_DAG_SPLIT)
+           pre (GPS_OPT_PRED_PRE), dag (GPS_OPT_DAG), dagt (GPS_OPT_DAG_TILES), fine (GPS_OPT_DAG_FINE)
 Variants are interleaved round-robin for --rounds rounds; prints the median ms/unit.
 """
 import argparse
@@ -24,7 +24,7 @@ from gpscore import _lib  # noqa: E402
 
 KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN,
         "graph": _lib.GPS_OPT_GRAPH, "tiny": _lib.GPS_OPT_TINY_GEMM, "pre": _lib.GPS_OPT_PRED_PRE,
-        "dag": _lib.GPS_OPT_DAG, "dagt": _lib.GPS_OPT_DAG_TILES, "forkmax": _lib.GPS_OPT_FORK_MAX, "arch": _lib.GPS_OPT_AR_CHUNKS, "sprio": 16, "dagg": _lib.GPS_OPT_DAG_GROUP, "sk": _lib.GPS_OPT_STREAM_K, "dagwg": _lib.GPS_OPT_DAG_WGS, "glds": _lib.GPS_OPT_GEMM_GLDS, "fine": _lib.GPS_OPT_DAG_FINE, "split": _lib.GPS_OPT_DAG_SPLIT, "prio": _lib.GPS_OPT_GEMM_PRIO, "order": _lib.GPS_OPT_DAG_ORDER, "sxcd": _lib.GPS_OPT_SLAB_XCD}
+        "dag": _lib.GPS_OPT_DAG, "dagt": _lib.GPS_OPT_DAG_TILES, "forkmax": _lib.GPS_OPT_FORK_MAX, "arch": _lib.GPS_OPT_AR_CHUNKS, "sprio": 16, "dagg": _lib.GPS_OPT_DAG_GROUP, "sk": _lib.GPS_OPT_STREAM_K, "dagwg": _lib.GPS_OPT_DAG_WGS, "fine": _lib.GPS_OPT_DAG_FINE, "prio": _lib.GPS_OPT_GEMM_PRIO, "order": _lib.GPS_OPT_DAG_ORDER, "sxcd": _lib.GPS_OPT_SLAB_XCD}
 
 
 def main():

@@ -2,7 +2,7 @@
 // of T 128-tiles, standalone: timing over repeated launches, a sampled correctness check
 // (L·Lᵀ = A and L⁻¹·L = I on random entries), and one traced launch whose per-slot timestamps
 // go to a CSV for tools/dag_trace.py (critical path, hand-off latencies, per-type durations).
-//   dag_bench [T=20] [nwg=256] [trace.csv|-] [reps=20] [group=3] [order=1] [fine=1] [split=0]
+//   dag_bench [T=20] [nwg=256] [trace.csv|-] [reps=20] [group=3] [order=1] [fine=1]
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -25,10 +25,9 @@ int main(int argc, char** argv) {
   const int group = argc > 5 ? atoi(argv[5]) : 3;
   const int order = argc > 6 ? atoi(argv[6]) : 1;
   const int fine = argc > 7 ? atoi(argv[7]) : 1;
-  const int split = argc > 8 ? atoi(argv[8]) : 0;
-  if (argc > 9) {  // order 1's weights: LEAF,fine,TRSM,UPD,UPDX,FIN,hand-off
+  if (argc > 8) {  // order 1's weights: LEAF,fine,TRSM,UPD,UPDX,FIN,hand-off
     double* w = gps::g_dag_weights;
-    if (sscanf(argv[9], "%lf,%lf,%lf,%lf,%lf,%lf,%lf", w, w + 1, w + 2, w + 3, w + 4, w + 5, w + 6) != 7) {
+    if (sscanf(argv[8], "%lf,%lf,%lf,%lf,%lf,%lf,%lf", w, w + 1, w + 2, w + 3, w + 4, w + 5, w + 6) != 7) {
       fprintf(stderr, "weights: 7 comma-separated numbers\n");
       return 2;
     }
@@ -45,7 +44,7 @@ int main(int argc, char** argv) {
       for (int k = 0; k < d; ++k) { const double t = X[i * d + k] - X[j * d + k]; s += t * t; }
       h[(size_t)i * n + j] = exp(-0.25 * s) + (i == j ? 0.05 : 0.0);
     }
-  const std::vector<uint32_t> tl = dag_task_list(T, order, fine != 0, split != 0);
+  const std::vector<uint32_t> tl = dag_task_list(T, order, fine != 0);
   const int nt = (int)tl.size();
   double *A0, *A, *Li, *ld;
   int *info, *cnt;
@@ -64,7 +63,7 @@ int main(int argc, char** argv) {
   DagParams p;
   p.A = A; p.lda = n; p.Linv = Li; p.ldl = n; p.Lout = nullptr; p.ldlo = 0;
   p.logdiag = ld; p.info = info; p.base = 0; p.nreal = n; p.T = T;
-  p.tasks = tasks; p.ntasks = nt; p.cnt = cnt; p.spin_ticks = 200000000ull; p.group = group; p.split = split;
+  p.tasks = tasks; p.ntasks = nt; p.cnt = cnt; p.spin_ticks = 200000000ull; p.group = group;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto launch = [&](bool tr, float* ms) {
@@ -116,7 +115,7 @@ int main(int argc, char** argv) {
   double lsum = 0;
   for (double x : gld) lsum += x;
   const double fl = 2.0 * n * (double)n * n / 3.0;
-  printf("group=%d order=%d fine=%d split=%d w=%s ", group, order, fine, split, argc > 9 ? argv[9] : "-");
+  printf("group=%d order=%d fine=%d w=%s ", group, order, fine, argc > 8 ? argv[8] : "-");
   printf("T=%d n=%d nwg=%d tasks=%d: median %.3f ms (min %.3f, max %.3f) = %.1f us/tile, %.2f TF/s; "
          "max|XAX^T - I| %.2e over 24 samples, sum log L_ii %.6f\n",
          T, n, nwg, nt, ts[ts.size() / 2], ts[0], ts.back(), 1e3 * ts[ts.size() / 2] / T,
