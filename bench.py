@@ -634,9 +634,9 @@ def c5_tol(Z, th):
 def host_gpu():
     try:
         import torch
-        return torch.cuda.get_device_name(0)
+        return torch.cuda.get_device_properties(0).name or "MI355X"
     except Exception:  # noqa: BLE001
-        return "unknown device"
+        return "one MI355X"
 
 
 def log(msg):

@@ -161,6 +161,9 @@ struct gps_ctx {
   // block-LOO scratch (per fold, reused): P, its L⁻¹ / P⁻¹ / H, vectors; full-GP Gblk, T;
   // FITC gradient: the fold's G_f, E_f, G_fE_f and F = Gblk E; energy score: work area, draws
   DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
+  // FITC block-LOO fold covariances (fitc_fold_cov): the folds' K_gᵀΛ_g⁻¹K_g slabs, B_{−f} and its
+  // L⁻¹ / log-diagonal, the remote ranks' sum, W_f = K_f L_{−f}⁻ᵀ, the fold's padded 1/λ
+  DBuf bSg, bBf, bLf, bldf, bRem, bW, bkv;
   DBuf ebuf_aux[3], bPIs, bRW;  // concurrent ES folds: work areas of the aux streams, C_f, r_f / w_f
   DBuf escale;                  // ES: per fold ‖C_f‖∞, then the row-sum scratch
   DBuf bfv;                       // sharded FITC block-LOO: row counts, then the fold values
@@ -1102,15 +1105,18 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   return 0;
 }
 
+// cform (FITC, round 5): getP writes the fold covariance C_f = P_f⁻¹ itself (full, padded as
+// diag(C_f, I)) into its P argument — blockloo_folds then passes C_f's buffer as P⁻¹ — and
+// −½log|C_f| into its last argument (the ½log|P_f| slot); no b×b factorisation or inverse.
 template <class GetP, class GDst, class GDone>
 int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective, const double* alpha,
                    const double* y, GetP getP, bool want_grad, GDst gdst, GDone gdone, double* g,
-                   const EsArgs* es, double* vals) {
+                   const EsArgs* es, double* vals, bool cform = false) {
   hipStream_t s = ctx->stream;
   const int nfold = (int)bnd.size() - 1;
   const int64_t bp = bounds_pad(bnd);
   HIPCHK(ensure(ctx, ctx->bP, (size_t)bp * bp * 8));
-  if (ctx->bL.cap < (size_t)bp * bp * 8 || !factor_zeroed(ctx, ctx->bL.d(), bp)) {
+  if (!cform && (ctx->bL.cap < (size_t)bp * bp * 8 || !factor_zeroed(ctx, ctx->bL.d(), bp))) {
     HIPCHK(ensure(ctx, ctx->bL, (size_t)bp * bp * 8));
     HIPCHK(zero_factor(ctx, ctx->bL.d(), bp, s));
   }
@@ -1148,20 +1154,28 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   HIPCHK(hipMemsetAsync(v, 0, (size_t)9 * bp * 8, s));
   for (int f = 0; f < nfold; ++f) {
     const int64_t a = bnd[f], b = bnd[f + 1] - bnd[f];
-    if ((rc = getP(f, a, b, ctx->bP.d(), bp))) return rc;
-    if ((rc = potrf_inv(ctx, ctx->bP.d(), bp, ctx->bL.d(), ctx->W.d(), ld, (int)b, nullptr)))
-      return rc;
-    HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
-    HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
-    HIPCHK(launch_gemv_lower(ctx->bL.d(), bp, af, t, (int)bp, s));
-    HIPCHK(launch_colred(ctx->bL.d(), bp, (int)bp, (int)bp, 1, t, nullptr, r, c, ctx->slab.d(), s));
-    HIPCHK(launch_dot(ld, nullptr, (int)b, fs + 3 * f, s));
+    if (cform) {  // C_f straight into the P⁻¹ buffer: r = C_fα_f, c = diag C_f
+      if ((rc = getP(f, a, b, ctx->bPI.d(), bp, fs + 3 * f))) return rc;
+      HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
+      HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
+      HIPCHK(launch_gemv_full(ctx->bPI.d(), bp, af, r, (int)bp, (int)bp, s));
+      HIPCHK(launch_pad_copy(ctx->bPI.d(), bp + 1, c, 1, (int)b, 1, (int)bp, 1, 0, s));
+    } else {
+      if ((rc = getP(f, a, b, ctx->bP.d(), bp, nullptr))) return rc;
+      if ((rc = potrf_inv(ctx, ctx->bP.d(), bp, ctx->bL.d(), ctx->W.d(), ld, (int)b, nullptr)))
+        return rc;
+      HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
+      HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
+      HIPCHK(launch_gemv_lower(ctx->bL.d(), bp, af, t, (int)bp, s));
+      HIPCHK(launch_colred(ctx->bL.d(), bp, (int)bp, (int)bp, 1, t, nullptr, r, c, ctx->slab.d(), s));
+      HIPCHK(launch_dot(ld, nullptr, (int)b, fs + 3 * f, s));
+    }
     HIPCHK(launch_dot(af, r, (int)b, fs + 3 * f + 1, s));
     if (kc)
       HIPCHK(launch_fold_terms(yf, r, c, (int)b, want_grad ? gm : nullptr, gc, fs + 3 * f + 2, s));
     if (!want_grad && !esq) continue;
     double* PI = es_conc ? PIs + (int64_t)f * bp * bp : ctx->bPI.d();
-    {  // C_f = P⁻¹ = Lp⁻ᵀLp⁻¹ (full)
+    if (!cform) {  // C_f = P⁻¹ = Lp⁻ᵀLp⁻¹ (full)
       GemmParams p = gp0();
       p.A = ctx->bL.d(); p.lda = bp; p.B = ctx->bL.d(); p.ldb = bp; p.C = PI; p.ldc = bp;
       p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.tri = TRI_K_GE_I; p.lower_out = 1;
@@ -1270,6 +1284,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
                  &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
+                 &ctx->bSg, &ctx->bBf, &ctx->bLf, &ctx->bldf, &ctx->bRem, &ctx->bW, &ctx->bkv,
                  &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->escale, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt};
 }
 
@@ -2577,7 +2592,7 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
     HIPCHK(launch_sym_mirror(ctx->A.d(), np, (int)np, s));
   }
   double* Ainv = ctx->A.d();
-  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bp) -> int {
+  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bp, double*) -> int {
     HIPCHK(launch_pad_copy(Ainv + a * np + a, np, P, bp, (int)b, (int)b, (int)bp, (int)bp, 1, s));
     return 0;
   };
@@ -2861,14 +2876,61 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     HIPCHK(hipMemsetAsync(gg, 0, (size_t)2 * np * 8, s));  // g and diag(Gblk)
   }
   HIPCHK(ensure(ctx, ctx->bT, (size_t)bp * mp * 8));
-  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bpp) -> int {
-    double* Uf = ctx->bT.d();
-    HIPCHK(launch_pad_copy(U + a * ldr, ldr, Uf, mp, (int)b, (int)mp, (int)bpp, (int)mp, 0, s));
+  // the fold covariances C_f = Λ_f + K_f B_{−f}⁻¹K_fᵀ (round 5, oracle.fitc_fold_cov): first every
+  // local fold's S_g = K_gᵀΛ_g⁻¹K_g (one SYRK over its rows); B_{−f} is then K̃mm + Σ_{g≠f} S_g
+  // (+ the other ranks' Σ S when sharded) — no subtraction of nearly equal b×b terms
+  const int nfl = (int)fid.size();
+  const int64_t mm = mp * mp;
+  HIPCHK(ensure(ctx, ctx->bSg, (size_t)nfl * mm * 8));
+  HIPCHK(ensure(ctx, ctx->bBf, (size_t)mm * 8));
+  HIPCHK(ensure(ctx, ctx->bldf, (size_t)mp * 8));
+  HIPCHK(ensure(ctx, ctx->bW, (size_t)bp * mp * 8));
+  HIPCHK(ensure(ctx, ctx->bkv, (size_t)bp * 8));
+  HIPCHK(ensure(ctx, ctx->W, std::max(ctx->W.cap, potrf_ws_doubles(mp) * 8)));
+  if (ctx->bLf.cap < (size_t)mm * 8 || !factor_zeroed(ctx, ctx->bLf.d(), mp)) {
+    HIPCHK(ensure(ctx, ctx->bLf, (size_t)mm * 8));
+    HIPCHK(zero_factor(ctx, ctx->bLf.d(), mp, s));
+  }
+  HIPCHK(hipMemsetAsync(ctx->bSg.p, 0, (size_t)nfl * mm * 8, s));  // (upper tiles stay zero)
+  for (int gl = 0; gl < nfl; ++gl) {
+    const int64_t a = bnd[gl], b = bnd[gl + 1] - bnd[gl];
+    HIPCHK(launch_pad_copy(ctx->Knm.d() + a * mp, mp, ctx->bT.d(), mp, (int)b, (int)mp, (int)bp,
+                           (int)mp, 0, s));
+    HIPCHK(launch_pad_copy(ctx->ilam.d() + a, 1, ctx->bkv.d(), 1, (int)b, 1, (int)bp, 1, 0, s));
     GemmParams p = gp0();
-    p.A = Uf; p.lda = mp; p.B = Uf; p.ldb = mp; p.C = P; p.ldc = bpp;
-    p.M = (int)bpp; p.N = (int)bpp; p.K = (int)mp; p.alpha = -1.0; p.lower_out = 1;
-    if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
-    HIPCHK(launch_add_diag(P, bpp, ctx->ilam.d() + a, (int)b, (int)bpp, s));
+    p.A = ctx->bT.d(); p.lda = mp; p.B = ctx->bT.d(); p.ldb = mp; p.C = ctx->bSg.d() + gl * mm;
+    p.ldc = mp; p.M = (int)mp; p.N = (int)mp; p.K = (int)bp; p.kscale = ctx->bkv.d(); p.lower_out = 1;
+    if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
+  }
+  const double* remote = nullptr;
+  if (shard) {  // the other ranks' folds: Σ_all S − Σ_local S (m×m; all-reduced once)
+    HIPCHK(ensure(ctx, ctx->bRem, (size_t)mm * 8));
+    HIPCHK(launch_fold_sum(ctx->bSg.d(), mm, nfl, -1, nullptr, nullptr, 1.0, ctx->bRem.d(), mm, s));
+    if ((rc = allreduce_sum(ctx, ctx->bRem.d(), (size_t)mm, s))) return rc;
+    HIPCHK(launch_fold_sum(ctx->bSg.d(), mm, nfl, -1, ctx->bRem.d(), nullptr, -1.0, ctx->bRem.d(), mm, s));
+    remote = ctx->bRem.d();
+  }
+  auto getP = [&](int fl, int64_t a, int64_t b, double* C, int64_t bpp, double* hl) -> int {
+    HIPCHK(launch_fold_sum(ctx->bSg.d(), mm, nfl, fl, ctx->Kmm.d(), remote, 1.0, ctx->bBf.d(), mm, s));
+    if (int rc2 = potrf_inv(ctx, ctx->bBf.d(), mp, ctx->bLf.d(), ctx->W.d(), ctx->bldf.d(), (int)m,
+                            nullptr))
+      return rc2;
+    HIPCHK(launch_pad_copy(ctx->Knm.d() + a * mp, mp, ctx->bT.d(), mp, (int)b, (int)mp, (int)bpp,
+                           (int)mp, 0, s));
+    {  // W_f = K_f L_{−f}⁻ᵀ
+      GemmParams p = gp0();
+      p.A = ctx->bT.d(); p.lda = mp; p.B = ctx->bLf.d(); p.ldb = mp; p.C = ctx->bW.d(); p.ldc = mp;
+      p.M = (int)bpp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+      if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
+    }
+    {  // C_f = W_f W_fᵀ (full) + Λ_f, padded as diag(C_f, I)
+      GemmParams p = gp0();
+      p.A = ctx->bW.d(); p.lda = mp; p.B = ctx->bW.d(); p.ldb = mp; p.C = C; p.ldc = bpp;
+      p.M = (int)bpp; p.N = (int)bpp; p.K = (int)mp; p.lower_out = 1; p.mirror = 1;
+      if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
+    }
+    HIPCHK(launch_add_diag(C, bpp, ctx->lam.d() + a, (int)b, (int)bpp, s));
+    HIPCHK(launch_fold_logdet(ctx->bldf.d(), ctx->ldb.d(), (int)m, ctx->lam.d() + a, (int)b, hl, s));
     return 0;
   };
   auto gdst = [&](int64_t, int64_t) { return std::make_pair(ctx->bG.d(), bp); };
@@ -2886,7 +2948,7 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
   };
   std::vector<double> fvl(fid.size()), fv((size_t)nfold, 0.0);
   if ((rc = blockloo_folds(ctx, bnd, objective, alpha, ctx->fy.d(), getP, want, gdst, gdone,
-                           want ? gg : nullptr, nullptr, fvl.data())))
+                           want ? gg : nullptr, nullptr, fvl.data(), true)))
     return rc;
   for (size_t j = 0; j < fid.size(); ++j) fv[fid[j]] = fvl[j];
   if (shard) {  // every fold's value on every rank (each fold is computed by exactly one rank)

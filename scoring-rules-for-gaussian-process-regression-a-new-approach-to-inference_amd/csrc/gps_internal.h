@@ -365,6 +365,12 @@ hipError_t launch_add_diag(double* P, int64_t ld, const double* vals, int nreal,
 hipError_t launch_row_scale(double* M, int64_t ld, int rows, int cols, const double* scale,
                             hipStream_t s);
 hipError_t launch_vec_mul(const double* a, const double* b, int n, double* out, hipStream_t s);
+// dst = base (+ base2) + sgn·Σ_{g ≠ skip} slab_g (len doubles, slabs `stride` apart, fixed order)
+hipError_t launch_fold_sum(const double* slab, int64_t stride, int nslab, int skip, const double* base,
+                           const double* base2, double sgn, double* dst, int64_t len, hipStream_t s);
+// *out = Σ ldf[<m] − Σ ldb[<m] − ½Σ log lam[<b]: −½log|C_f| of a FITC block-LOO fold covariance
+hipError_t launch_fold_logdet(const double* ldf, const double* ldb, int m, const double* lam, int b,
+                              double* out, hipStream_t s);
 // FITC block-LOO gradient (whitened): M_ii, the V Lm⁻¹ row scale and Y = −2Λ⁻¹F̃ + 2ŨS̃
 // (see kernels_block.hip; Y may alias US)
 hipError_t launch_blk_mdiag(const double* F, int64_t ldf, const double* US, int64_t ldus,

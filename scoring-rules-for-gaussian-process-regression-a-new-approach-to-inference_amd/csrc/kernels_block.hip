@@ -89,6 +89,49 @@ hipError_t launch_add_diag(double* P, int64_t ld, const double* vals, int nreal,
   return hipGetLastError();
 }
 
+// FITC block-LOO covariance (round 5, api.hip fitc_fold_cov): dst[e] = base[e] (+ base2[e]) +
+// sgn·Σ_{g ≠ skip} slab_g[e], the slabs in ascending order (fixed: bitwise reproducible); e < len
+__global__ __launch_bounds__(256) void fold_sum_kernel(const double* __restrict__ slab, int64_t stride,
+                                                       int nslab, int skip, const double* base,
+                                                       const double* base2, double sgn,
+                                                       double* dst, int64_t len) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= len) return;
+  double v = base ? base[e] : 0.0;
+  if (base2) v += base2[e];
+  for (int g = 0; g < nslab; ++g)
+    if (g != skip) v = fma(sgn, slab[g * stride + e], v);
+  dst[e] = v;
+}
+
+hipError_t launch_fold_sum(const double* slab, int64_t stride, int nslab, int skip, const double* base,
+                           const double* base2, double sgn, double* dst, int64_t len, hipStream_t s) {
+  hipLaunchKernelGGL(fold_sum_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, slab,
+                     stride, nslab, skip, base, base2, sgn, dst, len);
+  return hipGetLastError();
+}
+
+// *out = Σ_{i<m} ldf[i] − Σ_{i<m} ldb[i] − ½Σ_{i<b} log lam[i] = −½log|C_f| of the fold covariance
+// C_f = Λ_f + K_f B_{−f}⁻¹K_fᵀ (log|C_f| = Σ log λ_f + log|B| − log|B_{−f}|; ld* = log L_ii of
+// the two factors) — the P-sign convention of blockloo_folds' ½log|P_f| slot.  One workgroup.
+__global__ __launch_bounds__(256) void fold_logdet_kernel(const double* __restrict__ ldf,
+                                                          const double* __restrict__ ldb, int m,
+                                                          const double* __restrict__ lam, int b,
+                                                          double* __restrict__ out) {
+  __shared__ double sh[16];
+  double v[1] = {0.0};
+  for (int i = threadIdx.x; i < m; i += 256) v[0] += ldf[i] - ldb[i];
+  for (int i = threadIdx.x; i < b; i += 256) v[0] -= 0.5 * log(lam[i]);
+  block_sum<1>(v, sh);
+  if (threadIdx.x == 0) *out = v[0];
+}
+
+hipError_t launch_fold_logdet(const double* ldf, const double* ldb, int m, const double* lam, int b,
+                              double* out, hipStream_t s) {
+  hipLaunchKernelGGL(fold_logdet_kernel, dim3(1), dim3(256), 0, s, ldf, ldb, m, lam, b, out);
+  return hipGetLastError();
+}
+
 // M[i][:] *= scale[i] for i < rows (cols even)
 __global__ __launch_bounds__(256) void row_scale_kernel(double* __restrict__ M, int64_t ld, int rows,
                                                         int cols, const double* __restrict__ scale) {
