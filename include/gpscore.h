@@ -109,11 +109,13 @@ enum {
                              as workgroup slots free up; 0 (default): equal priority */
   GPS_OPT_DAG_TILES = 13, /* largest block (in 128-tiles, 2..64, default 20) the persistent
                             factorisation takes */
-  GPS_OPT_STREAM_K = 18,  /* 1: a 128-tile GEMM launch with uniform K ranges (the trailing-update
-                             SYRKs) whose last round of workgroup slots would be at most 3/4 full
-                             splits that round's tiles into equal K runs over every slot (in-launch
-                             fixed-order combine); 0 (default): one workgroup per tile — with the
-                             side-stream fork the tail is already filled.  Process-wide. */
+  GPS_OPT_STREAM_K = 18,  /* the stream-K tail of a 128-tile GEMM launch with uniform K ranges (the
+                             trailing-update SYRKs) whose last round of workgroup slots would be at
+                             most 3/4 full: that round's tiles split into equal K runs over every
+                             slot (in-launch fixed-order combine).  2 (default): for a trailing update
+                             that runs alone (overlap off, or below the fork level) — beside the side
+                             stream's T product the round is filled already; 1: every eligible
+                             launch; 0: never.  Process-wide. */
   GPS_OPT_DAG_WGS = 19,   /* workgroups of a persistent factorisation launch; 0 (default):
                              automatic — one per CU for the full GP, half the CUs for the FITC
                              m×m factorisations (the test pre-pass runs beside them) */

@@ -452,6 +452,7 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
   GemmParams p = gp0();
   p.A = ctx->Knm.d(); p.lda = mp; p.B = Lx + c0 * mp; p.ldb = mp;
   p.M = (int)np; p.N = (int)(c1 - c0); p.K = (int)c1; p.tri = TRI_K_LE_J; p.tri_off = (int)c0;
+  p.kend = (int)pad_to(ctx->m, 16);
   p.out0 = ctx->fslab.d() + (c0 / GPS_TILE) * np; p.ld_out = np;
   return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
@@ -546,10 +547,12 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     HIPCHK(hipEventRecord(fork, s));
     HIPCHK(hipStreamWaitEvent(ts, fork, 0));
   }
-  {  // trailing update A22 -= L21 L21ᵀ (lower tiles)
+  {  // trailing update A22 -= L21 L21ᵀ (lower tiles); alone (nothing forked) it takes the
+     // stream-K tail for its last round of workgroup slots
     GemmParams p = gp0();
     p.A = W; p.lda = n1; p.B = W; p.ldb = n1; p.C = A22; p.ldc = lda;
     p.M = n2; p.N = n2; p.K = n1; p.alpha = -1.0; p.beta = 1.0; p.lower_out = 1;
+    p.sk_alone = forked ? 0 : 1;
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p))) return rc;
   }
   {  // T = L21 · L11⁻¹ → A21 (off the critical path)
@@ -1402,7 +1405,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->ar_chunks = value;
       return 0;
     case GPS_OPT_TINY_GEMM: g_tiny_gemm = value != 0; return 0;
-    case GPS_OPT_STREAM_K: g_stream_k = value != 0; return 0;
+    case GPS_OPT_STREAM_K:
+      ARGCHK(value >= 0 && value <= 2, "GPS_OPT_STREAM_K must be 0, 1 or 2");
+      g_stream_k = value;
+      return 0;
     case GPS_OPT_SLAB_XCD: g_slab_xcd = value != 0; return 0;
     case GPS_OPT_GEMM_PRIO: g_gemm_prio = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
@@ -2107,7 +2113,7 @@ int fitc_test_prepass(gps_ctx* ctx) {
     return rc;
   GemmParams p = gp0();
   p.A = ctx->Ksm.d(); p.lda = mp; p.B = ctx->Lm.d(); p.ldb = mp;
-  p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+  p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J; p.kend = (int)pad_to(m, 16);
   p.out0 = ctx->fslab_pre.d(); p.ld_out = ntp;
   if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, a))) return rc;
   HIPCHK(launch_slab_sum(ctx->fslab_pre.d(), ntp, (int)tm, ntp, nullptr, ctx->qm.d(), a));
@@ -2129,6 +2135,7 @@ int fitc_test_prepass_b(gps_ctx* ctx) {
   GemmParams p = gp0();
   p.A = ctx->Ksm.d(); p.lda = mp; p.B = ctx->Lb.d(); p.ldb = mp;
   p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+  p.kend = (int)pad_to(ctx->m, 16);
   p.out0 = ctx->fslab_pre.d(); p.ld_out = ntp;  // (the q* slab sum precedes on aux[0])
   if (int rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, a)) return rc;
   HIPCHK(launch_slab_sum(ctx->fslab_pre.d(), ntp, (int)tm, ntp, nullptr, ctx->qb.d(), a));
@@ -2293,6 +2300,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d() + qn1 * mp; p.ldb = mp;
     p.M = (int)np; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
+    p.kend = (int)pad_to(m, 16);
     p.out0 = ctx->fslab.d() + (qn1 / GPS_TILE) * np; p.ld_out = np;
     p.w = ctx->c.d(); p.out1 = ctx->g.d();
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ_DOT, p))) return rc;
@@ -3115,6 +3123,7 @@ int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC])
     GemmParams p = gp0();
     p.A = ctx->Ksm.d(); p.lda = mp; p.B = Ls[w]; p.ldb = mp;
     p.M = (int)ntp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+    p.kend = (int)pad_to(ctx->m, 16);
     p.out0 = ctx->fslab.d(); p.ld_out = ntp;
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p))) return rc;
     HIPCHK(launch_slab_sum(ctx->fslab.d(), ntp, (int)tm, ntp, nullptr, outs[w], s));

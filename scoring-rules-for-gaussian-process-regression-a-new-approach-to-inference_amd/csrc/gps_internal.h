@@ -65,8 +65,7 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
                              // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto,
-                             // 5 XCD-banded 8×8 patches (auto for EPI_ROWSQ), 6 auto without 5,
-                             // 7 XCD-banded with the band index inner, 8 auto with 7 for EPI_ROWSQ
+                             // 5 XCD-banded 8×8 patches (auto for EPI_ROWSQ)
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
@@ -81,6 +80,14 @@ struct GemmParams {
                              // reduction when there is one, else by launch_sym_mirror)
   int slab_xcd;              // set by launch_gemm (g_slab_xcd): a split-K grid's (tile, slice)
                              // pairs dealt slice-major in contiguous runs per XCD
+  int kend;                  // > 0 (a multiple of 16): A's columns k >= kend are zero and B's rows
+                             // j >= kend its identity padding (the FITC row norms: kend = m rounded
+                             // to 16) — the K loop stops there and, for EPI_ROWSQ*, 16-column
+                             // blocks of such rows (and, TRI_K_LE_J, slices above a block's
+                             // diagonal) skip their MFMAs: exact zeros either way
+  int sk_alone;              // the launch runs without a concurrent forked product (potrf_inv_rec's
+                             // trailing update when nothing is forked beside it): the stream-K
+                             // tail fills its last round (GPS_OPT_STREAM_K = 2, the default)
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
@@ -88,7 +95,8 @@ struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
 extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
-extern int g_stream_k;   // 1: the stream-K tail of uniform-K 128-tile launches (launch_gemm)
+extern int g_stream_k;   // stream-K tail of uniform-K 128-tile launches (launch_gemm): 0 never,
+                         // 1 every eligible launch, 2 (default) those marked sk_alone
 extern int g_gemm_prio;  // s_setprio around the mainloop's MFMA phase: 0 off, 1 (default) products, 2 all
 extern int g_slab_xcd;   // split-K launches: each XCD runs whole K slices (GPS_OPT_SLAB_XCD)
 constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)

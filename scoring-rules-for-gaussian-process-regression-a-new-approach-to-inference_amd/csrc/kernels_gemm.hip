@@ -30,6 +30,8 @@
 // diagonal 128-blocks of a triangular factor are stored with explicit zeros
 // above the diagonal, so clipping at 64 or 128 granularity never drops a
 // nonzero) — no multiply touches a structurally zero tile.
+#include <climits>
+
 #include "gps_internal.h"
 
 namespace gps {
@@ -302,6 +304,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
       break;
     default: break;
   }
+  if (p.kend > 0 && ke > p.kend) ke = p.kend;  // (A's columns beyond kend are zero)
   if (kb_o >= 0) {  // a stream-K run: an explicit slice range of a uniform-K tile
     kb = kb_o;
     ke = ke_o;
@@ -387,7 +390,28 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
 #pragma unroll
     for (int ni = 0; ni < MI; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
 
-  auto compute = [&](int buf) {
+  // The FITC row norms (EPI_ROWSQ*, B = rows of a triangular L⁻¹, TRI_K_LE_J): a 16-column block of
+  // B whose rows lie in the identity padding (>= kend) or whose entries in this 16-deep slice are
+  // all above the rows' diagonal contributes exact zeros — its MFMAs are skipped (round 5: 12 % of
+  // the row norms' MFMAs at m = 2000, the m_pad padding and the zero halves of the diagonal blocks)
+  constexpr bool SKIP = EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT;
+  const int gcol = p.tri_off + col0 + wc * WT;  // global B row of the wave's first column block
+  const int kend_b = p.kend > 0 ? p.kend : INT_MAX;
+  auto active = [&](int k0) -> unsigned {
+    if constexpr (!SKIP) {
+      return (1u << MI) - 1;
+    } else {
+      unsigned m = 0;
+#pragma unroll
+      for (int ni = 0; ni < MI; ++ni) {
+        const int c = gcol + 16 * ni;
+        const bool on = c < kend_b && (p.tri != TRI_K_LE_J || k0 < c + 16);
+        m |= on ? 1u << ni : 0u;
+      }
+      return __builtin_amdgcn_readfirstlane(m);
+    }
+  };
+  auto compute = [&](int buf, unsigned act) {
     const double* As = smem + buf * STAGE;
     const double* Bs = As + BK * LS;
 #pragma unroll
@@ -402,7 +426,8 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < MI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+          if (act >> ni & 1)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
     }
   };
 
@@ -430,13 +455,13 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     for (int it = 0; it < nk - 1; ++it) {
       load_tile(kb + (it + 1) * BK);
       if (p.prio) __builtin_amdgcn_s_setprio(1);
-      compute(it & 1);
+      compute(it & 1, active(kb + it * BK));
       if (p.prio) __builtin_amdgcn_s_setprio(0);
       row_dot(it & 1, kb + it * BK);
       store_tile((it + 1) & 1);
       __syncthreads();
     }
-    compute((nk - 1) & 1);
+    compute((nk - 1) & 1, active(kb + (nk - 1) * BK));
     row_dot((nk - 1) & 1, kb + (nk - 1) * BK);
   }
   if constexpr (EPI == EPI_ROWSQ_DOT) {
@@ -732,7 +757,11 @@ int g_gemm_prio = 1;  // GPS_OPT_GEMM_PRIO (process-wide): s_setprio around the 
 // bytes 4.48 -> 1.91 GB per C4 launch (7x -> 2.9x its Knm operand), time neutral (C4 11.86 -> 11.83,
 // C3 / C5 within noise: profiles/r4_slab_xcd_ab.txt) — the SYRK is not fabric-bound
 int g_slab_xcd = 1;
-int g_stream_k = 0;   // GPS_OPT_STREAM_K (process-wide; off: DESIGN §6.20)
+// GPS_OPT_STREAM_K (process-wide): 2 (default) — the stream-K tail for launches that run alone (the
+// trailing update with nothing forked beside it: overlap off or below the fork level), where the
+// last round's idle slots are otherwise lost; with the side stream's T product beside the SYRK the
+// tail is already filled and the split only costs
+int g_stream_k = 2;
 
 // waves per output block of the small kernel: K split 4 ways whenever there are 4 chunks
 static int small_wpt(int K) { return K >= 64 ? 4 : (K >= 32 ? 2 : 1); }
@@ -861,7 +890,8 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // round of workgroup slots would be at most 3/4 full runs that round's tiles as equal K runs
   // over every slot instead
   q.sk_dp = q.sk_wgs = 0;
-  if (g_stream_k && epi == EPI_STORE && tile == 128 && q.ksplit == 1 && q.sk_cnt && q.ws &&
+  if ((g_stream_k == 1 || (g_stream_k == 2 && q.sk_alone)) && epi == EPI_STORE && tile == 128 &&
+      q.ksplit == 1 && q.sk_cnt && q.ws &&
       q.sk_slots > 0 && q.tri == TRI_NONE && (q.lower_out || q.map_mode == 0 || q.map_mode == 2)) {
     const int slots = q.sk_slots, rem = tiles % slots;
     if (tiles >= slots && rem > 0 && 4 * rem <= 3 * slots && rem <= kStreamKTiles &&
