@@ -10,3 +10,4 @@ F="-O3 --offload-arch=gfx950 -std=c++17 -I include -I $C -munsafe-fp-atomics -ml
 G=scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd/gpscore
 /opt/rocm/bin/hipcc $F tools/gemm_bench.cpp -L $G -lgpscore -Wl,-rpath,'$ORIGIN/../'$G -o tbin/gemm_bench &
 wait
+/opt/rocm/bin/hipcc $F tools/gram_bench.cpp -o tbin/gram_bench

@@ -1,0 +1,130 @@
+// Gram-build microbenchmark (round 5): the library's gram_reg_kernel<8> (csrc/kernels_gram.hip) on
+// the C3 shapes — K_ff lower (20000², d = 8) and K*f (5000 × 20000) — against variants of its
+// interior-tile loop on the K*f shape: store-only (the access pattern's ceiling), 256 columns per
+// workgroup, 64 rows per workgroup, 4 rows per unrolled step.  Bitwise check of each variant's
+// output against the library's.
+//   hipcc -O3 --offload-arch=gfx950 -I include -I <pkg>/csrc tools/gram_bench.cpp -o tbin/gram_bench
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+#include <vector>
+
+#include "kernels_gram.hip"
+using namespace gps;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+// interior-tile variant: ROWS × COLS tile, COLS / 128 column pairs per lane, UNR rows per step
+template <int D, int COLS, int ROWS, int UNR, bool STORE_ONLY>
+__global__ __launch_bounds__(256) void gram_var(GramParams p) {
+  constexpr int CP = COLS / 128;  // column pairs per lane
+  __shared__ __attribute__((aligned(16))) double xs_row[ROWS * D];
+  __shared__ double2 etab[64];
+  const int tiles_x = p.N / COLS;
+  const int c0 = (blockIdx.x % tiles_x) * COLS, r0 = (blockIdx.x / tiles_x) * ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < ROWS * D; e += 256) {
+    const int i = e / D, k = e - i * D;
+    xs_row[e] = p.x[(int64_t)(r0 + i) * D + k] * p.inv_ell[k];
+  }
+  double f[CP][2][D];
+#pragma unroll
+  for (int c = 0; c < CP; ++c)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < D; ++k) f[c][h][k] = p.xp[(int64_t)(c0 + 128 * c + 2 * lane + h) * D + k] * p.inv_ell[k];
+  exp_tab_stage(etab);
+  __syncthreads();
+#pragma unroll UNR
+  for (int rr = wave; rr < ROWS; rr += 4) {
+#pragma unroll
+    for (int c = 0; c < CP; ++c) {
+      double a0 = 0.0, a1 = 0.0;
+      if constexpr (!STORE_ONLY) {
+#pragma unroll
+        for (int k = 0; k < D; k += 2) {
+          const double2 xr = *reinterpret_cast<const double2*>(&xs_row[rr * D + k]);
+          double e0 = xr.x - f[c][0][k], e1 = xr.x - f[c][1][k];
+          a0 = fma(e0, e0, a0);
+          a1 = fma(e1, e1, a1);
+          e0 = xr.y - f[c][0][k + 1];
+          e1 = xr.y - f[c][1][k + 1];
+          a0 = fma(e0, e0, a0);
+          a1 = fma(e1, e1, a1);
+        }
+      }
+      double* dst = p.out + (int64_t)(r0 + rr) * p.ldo + c0 + 128 * c + 2 * lane;
+      if constexpr (STORE_ONLY)
+        st_nt2(dst, p.sf2, p.sf2);
+      else
+        st_nt2(dst, p.sf2 * exp_neg(-0.5 * a0, etab), p.sf2 * exp_neg(-0.5 * a1, etab));
+    }
+  }
+}
+
+int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);
+  const int d = 8, n = 20096, nt = 5120;  // padded C3 sizes (all tiles interior for K*f)
+  std::mt19937_64 rng(3);
+  std::normal_distribution<double> nd;
+  std::vector<double> hx((size_t)n * d), ht((size_t)nt * d);
+  for (auto& v : hx) v = nd(rng);
+  for (auto& v : ht) v = nd(rng);
+  double *X, *Xt, *out, *ref;
+  CK(hipMalloc(&X, hx.size() * 8)); CK(hipMalloc(&Xt, ht.size() * 8));
+  CK(hipMalloc(&out, (size_t)n * n * 8)); CK(hipMalloc(&ref, (size_t)nt * n * 8));
+  CK(hipMemcpy(X, hx.data(), hx.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(Xt, ht.data(), ht.size() * 8, hipMemcpyHostToDevice));
+  GramParams g;
+  memset(&g, 0, sizeof(g));
+  g.d = d; g.sf2 = 1.0;
+  for (int k = 0; k < d; ++k) g.inv_ell[k] = 0.5;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  auto time = [&](auto launch, double bytes, const char* name) {
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipDeviceSynchronize());
+    const int reps = 20;
+    CK(hipEventRecord(e0, 0));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    printf("%-34s %8.4f ms  %6.0f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+  };
+  // library: K_ff lower (n × n) and K*f (nt × n)
+  GramParams kff = g;
+  kff.x = X; kff.xp = X; kff.out = out; kff.ldo = n; kff.n = n; kff.m = n; kff.M = n; kff.N = n;
+  kff.lower = 1; kff.diag_add = 0.01; kff.pad_identity = 1;
+  time([&] { CK(launch_gram(kff, 0)); }, 8.0 * n * (n + 1.0) / 2, "library K_ff lower 20096^2");
+  GramParams ksf = g;
+  ksf.x = Xt; ksf.xp = X; ksf.out = ref; ksf.ldo = n; ksf.n = nt; ksf.m = n; ksf.M = nt; ksf.N = n;
+  time([&] { CK(launch_gram(ksf, 0)); }, 8.0 * nt * n, "library K*f 5120 x 20096");
+  const double bsf = 8.0 * nt * n;
+  GramParams v = ksf;
+  v.out = out;
+  auto check = [&](const char* name) {
+    std::vector<double> a((size_t)nt * n), b((size_t)nt * n);
+    CK(hipMemcpy(a.data(), out, a.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), ref, b.size() * 8, hipMemcpyDeviceToHost));
+    printf("    %s: %s\n", name, memcmp(a.data(), b.data(), a.size() * 8) ? "DIFFERS" : "bitwise equal");
+  };
+#define VAR(COLS, ROWS, UNR, SO, NAME)                                                           \
+  time([&] { hipLaunchKernelGGL((gram_var<8, COLS, ROWS, UNR, SO>),                             \
+                                dim3((nt / ROWS) * (n / COLS)), dim3(256), 0, 0, v); }, bsf, NAME); \
+  if (!SO) check(NAME);
+  VAR(128, 128, 2, true, "store-only 128x128");
+  VAR(128, 128, 2, false, "variant 128x128 unroll 2 (=lib)");
+  VAR(128, 128, 4, false, "variant 128x128 unroll 4");
+  VAR(128, 64, 2, false, "variant 64 rows x 128");
+  VAR(128, 256, 2, false, "variant 256 rows x 128");
+  if (n % 256 == 0) { VAR(256, 128, 2, false, "variant 128 x 256 cols"); }
+  return 0;
+}
