@@ -76,7 +76,8 @@ enum {
   GPS_OPT_OVERLAP = 0,  /* 1 (default): the factorisation's off-critical-path products (and the
                            energy score's folds) run on extra HIP streams; 0: everything on one
                            stream (clean per-kernel timing) */
-  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 fixed orders
+  GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 fixed orders, 6 the
+                           row norms in paired column tiles (other launches automatic)
                            (A/B measurements; same values bitwise) */
   GPS_OPT_FORK_MIN = 4, /* smallest recursion block (in 128-row blocks, default 1) whose
                            off-critical-path product is forked to the side stream */

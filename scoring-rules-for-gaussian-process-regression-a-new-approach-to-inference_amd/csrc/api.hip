@@ -1378,7 +1378,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
   switch (key) {
     case GPS_OPT_OVERLAP: ctx->overlap = value != 0; return 0;
     case GPS_OPT_GEMM_MAP:
-      ARGCHK(value >= 0 && value <= 5, "GPS_OPT_GEMM_MAP must be in 0..5");
+      ARGCHK(value >= 0 && value <= 6, "GPS_OPT_GEMM_MAP must be in 0..6");
       ctx->gemm_map = value;
       return 0;
     case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;

@@ -30,6 +30,7 @@ struct GramParams {
   int lower;          // write only j <= i (tile-granular skip + element mask)
   int pad_identity;   // 1.0 on the padded diagonal (i == j >= n)
   double inv_ell[GPS_MAX_D];
+  int edge;           // (launch_gram) the diagonal-tile launch of a d = 16 build (kernels_gram.hip)
 };
 
 enum Layout { LAY_N = 0, LAY_T = 1 };

@@ -147,6 +147,24 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       return;
     }
   }
+  if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
+    if (p.map_mode == 6) {
+      // paired column tiles (row norms over a triangular L⁻¹, work ∝ tj + 1): workgroup (ti, q)
+      // runs column tile T−1−q and then q, so every workgroup has the same K, (T + 1)·TILE — the
+      // grid is uniform like a square product's — in a grouped raster over XCD-contiguous ids
+      const int np = (p.tiles_n + 1) >> 1;
+      const int l = xcd_remap(blockIdx.x, gridDim.x);
+      const int per_group = GROUP_M * np, g = l / per_group, first = g * GROUP_M;
+      const int gm = min(GROUP_M, p.tiles_m - first), tt = l - g * per_group;
+      const int ri = first + tt % gm, q = tt / gm, qh = p.tiles_n - 1 - q;
+      gemm_tile<ALAY, BLAY, EPI, TILE>(p, ri, qh, 0, smem);
+      if (q < qh) {
+        __syncthreads();  // (the first tile's reduction still reads the LDS the second stages into)
+        gemm_tile<ALAY, BLAY, EPI, TILE>(p, ri, q, 0, smem);
+      }
+      return;
+    }
+  }
   int ti, tj;
   if (p.slab_xcd) {
     // split-K, slice-major per XCD: the grid's (tile, slice) pairs in slice-major order, each XCD
@@ -867,14 +885,23 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   q.tiles_n = q.N / tile;
   int tiles = (int)tiles_for(q, tile);
   // triangular operands default to the XCD-banded heaviest-first order (map 3):
-  // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build; the
-  // FITC row norms (EPI_ROWSQ) to its 8×8-patch form (map 5): C5 174.0 vs 181.5 ms, while the
-  // patch order on the factorisation / predictive TRMMs cost C3 27 % (profiles/r2_map5_ab.txt)
-  // (the row norms in map 3 or in panel-inner bands measured slower in the library on C4 or C5:
-  // profiles/r4_rowsq_map_ab.txt)
+  // measured +2-4% over plain heaviest-first on every 10k-level shape of the C3 build.  The FITC
+  // row norms (EPI_ROWSQ*) over a triangular L⁻¹ default to paired column tiles (map 6: uniform
+  // work per workgroup; C4 11.82 → 11.72 ms, C5 neutral, profiles/r5h_rowsq_pairs.txt), before
+  // that to the 8×8-patch order (map 5: C5 174.0 vs 181.5 ms against map 3 in round 2, while the
+  // patch order on the factorisation / predictive TRMMs cost C3 27 %, profiles/r2_map5_ab.txt;
+  // maps 3 and 7 for the row norms: profiles/r4_rowsq_map_ab.txt)
+  const bool rowsq = epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT;
+  const bool pairable = rowsq && q.tri == TRI_K_LE_J && tile == 128 && q.ksplit == 1;
+  if (q.map_mode == 6 && !pairable) q.map_mode = 0;  // (an override of 6 leaves the rest automatic)
+  // pairs only with ≥ 4 rounds of the 512 workgroup slots: the uniform grid quantises — C4's
+  // test-side norms (79 × 8 pairs, 1.2 rounds) ran 1097 µs paired against 961 in map 5
+  // (profiles/r5k_rowsq_pairs_prof.txt)
+  const bool paired = pairable && (int64_t)q.tiles_m * ((q.tiles_n + 1) / 2) >= 2048;
   if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out)
-    q.map_mode = (epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT) ? 5 : 3;
+    q.map_mode = rowsq ? (paired ? 6 : 5) : 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)
+  if (q.map_mode == 6) tiles = q.tiles_m * ((q.tiles_n + 1) / 2);
   if (q.map_mode == 5 && (q.lower_out || q.tri == TRI_NONE || q.tri == TRI_KR_J)) q.map_mode = 0;
   if (q.map_mode == 5) {  // 8 XCDs × ceil(work / 8) groups × the band's 8-wide groups × 64
     const bool wi = q.tri == TRI_K_LE_I || q.tri == TRI_K_GE_I;

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
   }
 }
 
-// Register-resident variant for the compiled feature counts (d = 1, 8, 16): a 128×128
+// Register-resident variant for the compiled feature counts d = 1, 8 (16: gram_col_kernel): a 128×128
 // tile per workgroup, each lane holds its two columns' scaled features in VGPRs for the
 // whole tile and the 128 rows' scaled features sit in LDS, read as wave-uniform
 // (broadcast) 16-byte loads.  Per element that is 2d VALU ops + exp and no per-element
@@ -107,13 +107,27 @@ __global__ __launch_bounds__(256) void gram_kernel(GramParams p) {
 // arithmetic in the same order as gram_kernel: bitwise-identical output.
 constexpr int G2_ROWS = 128;
 
+// The d = 16 build in two launches: gram_col_kernel takes every tile but the diagonal ones when
+// something happens on i == j (a diagonal add, the identity padding, the lower mask) — those few
+// (one per tile row, Kmm / a lower K_ff only) go to gram_reg_kernel<16> over a compact grid.
+__host__ __device__ inline bool gram_diag_special(const GramParams& p) {
+  return p.diag_add != 0.0 || p.pad_identity || p.lower;
+}
+__host__ __device__ inline int64_t gram_edge_count(const GramParams& p) {
+  const int tx = p.N / GR_COLS, ty = (p.M + G2_ROWS - 1) / G2_ROWS;
+  return gram_diag_special(p) ? (tx < ty ? tx : ty) : 0;
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
   __shared__ __attribute__((aligned(16))) double xs_row[G2_ROWS * D];
   __shared__ double2 etab[64];
   const int tiles_x = p.N / GR_COLS;
-  const int bx = blockIdx.x % tiles_x;
-  const int by = blockIdx.x / tiles_x;
+  int bx = blockIdx.x % tiles_x;
+  int by = blockIdx.x / tiles_x;
+  if constexpr (D == 16) {  // (only the d = 16 build has an edge launch: the diagonal tiles)
+    if (p.edge) bx = by = blockIdx.x;
+  }
   const int c0 = bx * GR_COLS, r0 = by * G2_ROWS;
   if (p.lower && c0 > r0 + G2_ROWS - 1) return;
   const int rows = min(G2_ROWS, p.M - r0);
@@ -199,6 +213,58 @@ __global__ __launch_bounds__(256) void gram_reg_kernel(GramParams p) {
   }
 }
 
+// d = 16: the same 128×128 tile with ONE column per lane — waves 0 / 1 own columns 0-63 / 64-127
+// of the even rows, waves 2 / 3 of the odd rows — so a lane holds 16 features instead of 32 (60
+// VGPRs instead of 122: 8 waves per SIMD instead of 4) and stores 8 bytes per row.  Padded rows
+// and columns are zero-filled here; the diagonal tiles of a build with a diagonal add, identity
+// padding or the lower mask (Kmm, a lower K_ff) go to gram_reg_kernel<16> in a second launch of
+// one workgroup per tile row (with those selects in this kernel it needed 78 VGPRs, or spilled at
+// 64, and a kernel with scratch ran slower everywhere).  C5-shaped Knm (100096 × 4096) 2.85 →
+// 3.34 TB/s (profiles/r5i_gram_cols.txt; at d = 8 the two-column kernel is as fast).  Same
+// arithmetic in the same order: bitwise-identical output.
+template <int D>
+__global__ __launch_bounds__(256) void gram_col_kernel(GramParams p) {
+  __shared__ __attribute__((aligned(16))) double xs_row[G2_ROWS * D];
+  __shared__ double2 etab[64];
+  const int tiles_x = p.N / GR_COLS;
+  const int bx = blockIdx.x % tiles_x;
+  const int by = blockIdx.x / tiles_x;
+  if ((p.lower && bx > by) || (bx == by && gram_diag_special(p))) return;
+  const int c0 = bx * GR_COLS, r0 = by * G2_ROWS;
+  const int rows = min(G2_ROWS, p.M - r0);
+  const int tid = threadIdx.x;
+  for (int e = tid; e < rows * D; e += 256) {
+    const int i = e / D, k = e - i * D;
+    const int gi = r0 + i;
+    xs_row[e] = gi < p.n ? p.x[(int64_t)gi * D + k] * p.inv_ell[k] : 0.0;
+  }
+  const int gj = c0 + (tid & (GR_COLS - 1)), half = tid >> 7;
+  const bool colpad = gj >= p.m;
+  double f[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k)  // (a padded column reads the last real one; its outputs are 0)
+    f[k] = p.xp[(int64_t)(colpad ? p.m - 1 : gj) * D + k] * p.inv_ell[k];
+  exp_tab_stage(etab);
+  __syncthreads();
+  const int rend = min(rows, p.n - r0);  // real rows of the tile; the padded ones below get 0
+#pragma unroll 2
+  for (int rr = half; rr < rend; rr += 2) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; k += 2) {
+      const double2 xr = *reinterpret_cast<const double2*>(&xs_row[rr * D + k]);
+      double e = xr.x - f[k];
+      a = fma(e, e, a);
+      e = xr.y - f[k + 1];
+      a = fma(e, e, a);
+    }
+    const double v = p.sf2 * exp_neg(-0.5 * a, etab);
+    __builtin_nontemporal_store(colpad ? 0.0 : v, p.out + (int64_t)(r0 + rr) * p.ldo + gj);
+  }
+  for (int rr = max(rend, 0) + ((max(rend, 0) & 1) != half ? 1 : 0); rr < rows; rr += 2)
+    p.out[(int64_t)(r0 + rr) * p.ldo + gj] = 0.0;
+}
+
 int g_gram_reg = 1;  // GPS_OPT_GRAM_REG (process-wide; 0 = the LDS-column kernel for every d)
 
 hipError_t launch_gram(const GramParams& p, hipStream_t s) {
@@ -211,7 +277,14 @@ hipError_t launch_gram(const GramParams& p, hipStream_t s) {
     switch (p.d) {
       case 1: hipLaunchKernelGGL(gram_reg_kernel<1>, grid, block, 0, s, p); break;
       case 8: hipLaunchKernelGGL(gram_reg_kernel<8>, grid, block, 0, s, p); break;
-      default: hipLaunchKernelGGL(gram_reg_kernel<16>, grid, block, 0, s, p); break;
+      default: {
+        hipLaunchKernelGGL(gram_col_kernel<16>, grid, block, 0, s, p);
+        GramParams q = p;
+        q.edge = 1;
+        const int64_t e = gram_edge_count(p);
+        if (e > 0) hipLaunchKernelGGL(gram_reg_kernel<16>, dim3((unsigned)e), block, 0, s, q);
+        break;
+      }
     }
     return hipGetLastError();
   }

@@ -440,14 +440,15 @@ def test_not_positive_definite_raises(gp):
 
 # ------------------------------------------------------------------- L1 blocks
 @pytest.mark.parametrize("d", [1, 8, 16])
-@pytest.mark.parametrize("uplo", [0, 1])
-def test_gram_reg_kernel_bitwise(gpu_ctx, d, uplo):
-    """The register-resident Gram kernel (d in {1, 8, 16}) against the LDS-column kernel:
-    same arithmetic in the same order, so bitwise-identical output, including the padded
-    rows/columns (n, m not multiples of 128), the lower mask and the diagonal add."""
+@pytest.mark.parametrize("n,m,uplo", [(333, 201, 0), (333, 333, 1), (700, 520, 0), (640, 640, 1),
+                                      (1000, 384, 0), (521, 521, 1)])
+def test_gram_reg_kernel_bitwise(gpu_ctx, d, n, m, uplo):
+    """The register-resident Gram kernels (d in {1, 8, 16}; at d = 16 the one-column interior
+    kernel plus the compact edge launch) against the LDS-column kernel: same arithmetic in the same
+    order, so bitwise-identical output, including the padded rows/columns (n, m not multiples of
+    128, and exact multiples), the lower mask and the diagonal add."""
     from gpscore._lib import GPS_ARD, ptr
     rng = np.random.default_rng(10 + d)
-    n, m = 333, 333 if uplo else 201
     x = rng.standard_normal((n, d))
     xp = x if uplo else rng.standard_normal((m, d))
     ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
@@ -839,6 +840,17 @@ def test_gemm_slab_xcd_bitwise(gpu_ctx):
         gpu_ctx.call("gps_ctx_set_option", 26, 1)
     for a, b in zip(sx, base):
         assert np.array_equal(a, b)
+    # GPS_OPT_GEMM_MAP (3) 6: the FITC row norms in paired column tiles (one workgroup runs column
+    # tiles T-1-q and q) — again only the workgroup changes, every tile's K loop is the same
+    from gpscore import _lib
+    for mm in (6, 5):
+        try:
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_GEMM_MAP, mm)
+            alt = run()
+        finally:
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_GEMM_MAP, 0)
+        for a, b in zip(alt, base):
+            assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("n,tiles", [(2560, 20), (4000, 40)])

@@ -253,13 +253,52 @@ static int rowsq_study(double* A, double* B, double* o0) {
     {"C5/2    100096x4096", 100096, 4096}};
   GemmParams p; memset(&p, 0, sizeof(p));
   for (auto& c : cs)
-    for (int mm : {0, 6, 7, 1}) {  // auto (5), 3, 7, grouped raster
+    for (int mm : {0, 3, 1}) {  // auto (5), 3, grouped raster
       p.A = A; p.B = B; p.out0 = o0; p.alpha = 1.0; p.ksplit = 1; p.tile = 0;
       p.lda = c.N; p.ldb = c.N; p.ld_out = c.M;
       p.M = c.M; p.N = c.N; p.K = c.N; p.tri = TRI_K_LE_J; p.map_mode = mm;
       const double fl = (double)c.M * c.N * c.N;
       printf("rowsq %-22s map%d %7.2f TF/s\n", c.name, mm, run(LAY_N, LAY_T, EPI_ROWSQ, p, 5, fl));
     }
+  return 0;
+}
+
+// where the row norms lose against the square products: the C4 fit shape as row norms and as a
+// stored product, triangular K and full K, against the square 10k shape in both epilogues
+static int rowsq_iso(double* A, double* B, double* C, double* o0) {
+  struct S { const char* name; int M, N, epi, tri, mm; } cs[] = {
+    {"C4fit rowsq tri map5", 40064, 2048, EPI_ROWSQ, TRI_K_LE_J, 0},
+    {"C4fit rowsq tri map3", 40064, 2048, EPI_ROWSQ, TRI_K_LE_J, 3},
+    {"C4fit rowsq tri map6", 40064, 2048, EPI_ROWSQ, TRI_K_LE_J, 6},
+    {"C4pred rowsq tri map5", 10112, 2048, EPI_ROWSQ, TRI_K_LE_J, 0},
+    {"C4pred rowsq tri map6", 10112, 2048, EPI_ROWSQ, TRI_K_LE_J, 6},
+    {"C5/2 rowsq tri map5", 100096, 4096, EPI_ROWSQ, TRI_K_LE_J, 0},
+    {"C5/2 rowsq tri map6", 100096, 4096, EPI_ROWSQ, TRI_K_LE_J, 6},
+    {"C4fit rowsq full", 40064, 2048, EPI_ROWSQ, TRI_NONE, 0},
+    {"C4fit store tri map5", 40064, 2048, EPI_STORE, TRI_K_LE_J, 5},
+    {"C4fit store tri map3", 40064, 2048, EPI_STORE, TRI_K_LE_J, 3},
+    {"C4fit store full", 40064, 2048, EPI_STORE, TRI_NONE, 0},
+    {"10k rowsq tri map5", 10112, 9984, EPI_ROWSQ, TRI_K_LE_J, 0},
+    {"10k rowsq tri map3", 10112, 9984, EPI_ROWSQ, TRI_K_LE_J, 3},
+    {"10k rowsq tri map6", 10112, 9984, EPI_ROWSQ, TRI_K_LE_J, 6},
+    {"10k store tri map3", 10112, 9984, EPI_STORE, TRI_K_LE_J, 3},
+    {"10k store tri map0", 10112, 9984, EPI_STORE, TRI_K_LE_J, 0},
+  };
+  GemmParams p;
+  const int nc = sizeof(cs) / sizeof(cs[0]);
+  for (int pass = 0; pass < 3; ++pass)  // forward, reversed, forward: clock ramp and drift show
+  for (int ci = 0; ci < nc; ++ci)
+    for (int prio = 0; prio < 2; ++prio) {
+      const S& c = cs[pass == 1 ? nc - 1 - ci : ci];
+      memset(&p, 0, sizeof(p));
+      p.A = A; p.B = B; p.C = C; p.out0 = o0; p.alpha = 1.0; p.ksplit = 1; p.tile = 0;
+      p.lda = c.N; p.ldb = c.N; p.ldc = c.N; p.ld_out = c.M;
+      p.M = c.M; p.N = c.N; p.K = c.N; p.tri = c.tri; p.map_mode = c.mm;
+      g_gemm_prio = prio ? 2 : 0;
+      const double fl = (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.N;
+      printf("p%d %-24s prio%d %7.2f TF/s\n", pass, c.name, prio, run(LAY_N, LAY_T, c.epi, p, 5, fl));
+    }
+  g_gemm_prio = 1;
   return 0;
 }
 
@@ -314,6 +353,7 @@ int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "syrk")) return syrk_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "layout")) return layout_study(A, B, C);
   if (argc > 1 && !strcmp(argv[1], "rowsq")) return rowsq_study(A, B, o0);
+  if (argc > 1 && !strcmp(argv[1], "rowsq_iso")) return rowsq_iso(A, B, C, o0);
   if (argc > 1 && !strcmp(argv[1], "fsyrk")) return fsyrk_study(A, C, w);
   if (argc > 1 && !strcmp(argv[1], "sweep")) {
     double* ws; hipMalloc(&ws, (int64_t)8 * 5120 * 5120 * 8);

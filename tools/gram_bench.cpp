@@ -67,8 +67,137 @@ __global__ __launch_bounds__(256) void gram_var(GramParams p) {
   }
 }
 
-int main() {
+
+// One column per lane (the library keeps two: at d = 16 that is 64 VGPRs of features, 122 in all,
+// 4 waves per SIMD); the expansion form ‖x‖² + ‖z‖² − 2x·z drops the per-feature subtraction
+// (reported as max |diff| against the library: it is not the library's arithmetic).  ROWS rows
+// per workgroup, UNR rows per unrolled step.
+template <int D, bool EXPAND, int UNR, int ROWS>
+__global__ __launch_bounds__(256) void gram_one_col(GramParams p) {
+  __shared__ __attribute__((aligned(16))) double xs_row[ROWS * D];
+  __shared__ double rn[ROWS];
+  __shared__ double2 etab[64];
+  const int tiles_x = p.N / GR_COLS;
+  const int c0 = (blockIdx.x % tiles_x) * GR_COLS, r0 = (blockIdx.x / tiles_x) * ROWS;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < ROWS * D; e += 256) {
+    const int i = e / D, k = e - i * D;
+    xs_row[e] = p.x[(int64_t)(r0 + i) * D + k] * p.inv_ell[k];
+  }
+  const int gj = c0 + (tid & 127), half = tid >> 7;
+  double f[D], fn = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    f[k] = p.xp[(int64_t)gj * D + k] * p.inv_ell[k];
+    fn = fma(f[k], f[k], fn);
+  }
+  exp_tab_stage(etab);
+  __syncthreads();
+  if (EXPAND) {
+    for (int r = tid; r < ROWS; r += 256) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) s = fma(xs_row[r * D + k], xs_row[r * D + k], s);
+      rn[r] = s;
+    }
+    __syncthreads();
+  }
+  // waves 0 / 1 hold columns 0-63 / 64-127 for the even rows, waves 2 / 3 for the odd rows
+#pragma unroll UNR
+  for (int rr = half; rr < ROWS; rr += 2) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; k += 2) {
+      const double2 xr = *reinterpret_cast<const double2*>(&xs_row[rr * D + k]);
+      if (EXPAND) {
+        a = fma(xr.x, f[k], a);
+        a = fma(xr.y, f[k + 1], a);
+      } else {
+        double e = xr.x - f[k];
+        a = fma(e, e, a);
+        e = xr.y - f[k + 1];
+        a = fma(e, e, a);
+      }
+    }
+    if (EXPAND) a = fmax(fma(-2.0, a, rn[rr] + fn), 0.0);
+    __builtin_nontemporal_store(p.sf2 * exp_neg(-0.5 * a, etab), p.out + (int64_t)(r0 + rr) * p.ldo + gj);
+  }
+}
+
+__global__ void maxdiff_k(const double* a, const double* b, int64_t n, double* out) {
+  double m = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmax(m, fabs(a[i] - b[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) out[blockIdx.x * 4 + threadIdx.x / 64] = m;
+}
+
+// plain (interior) Gram of n × m at feature count D: the library against the one-column variants
+template <int D>
+static void col_study(int n, int m) {
+  std::mt19937_64 rng(5);
+  std::normal_distribution<double> nd;
+  std::vector<double> hx((size_t)n * D), hz((size_t)m * D);
+  for (auto& v : hx) v = nd(rng);
+  for (auto& v : hz) v = nd(rng);
+  double *X, *Zp, *ref, *out, *md;
+  CK(hipMalloc(&X, hx.size() * 8)); CK(hipMalloc(&Zp, hz.size() * 8));
+  CK(hipMalloc(&ref, (size_t)n * m * 8)); CK(hipMalloc(&out, (size_t)n * m * 8)); CK(hipMalloc(&md, 1024 * 8));
+  CK(hipMemcpy(X, hx.data(), hx.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(Zp, hz.data(), hz.size() * 8, hipMemcpyHostToDevice));
+  GramParams g;
+  memset(&g, 0, sizeof(g));
+  g.d = D; g.sf2 = 1.3; g.x = X; g.xp = Zp; g.ldo = m; g.n = n; g.m = m; g.M = n; g.N = m;
+  for (int k = 0; k < D; ++k) g.inv_ell[k] = 1.0 / (2.0 + 0.1 * k);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const double bytes = 8.0 * n * m;
+  auto time = [&](auto launch, const char* name) {
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipDeviceSynchronize());
+    const int reps = 10;
+    CK(hipEventRecord(e0, 0));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    printf("d%-2d %6d x %5d %-34s %8.4f ms  %6.0f GB/s\n", D, n, m, name, ms, bytes / (ms * 1e-3) / 1e9);
+  };
+  GramParams r = g; r.out = ref;
+  time([&] { CK(launch_gram(r, 0)); }, "library");
+  GramParams v = g; v.out = out;
+  auto check = [&](const char* name) {
+    hipLaunchKernelGGL(maxdiff_k, dim3(256), dim3(256), 0, 0, out, ref, (int64_t)n * m, md);
+    std::vector<double> h(1024);
+    CK(hipMemcpy(h.data(), md, 1024 * 8, hipMemcpyDeviceToHost));
+    double mx = 0.0;
+    for (double x : h) mx = fmax(mx, x);
+    printf("    %s: max |diff| vs library %.3e\n", name, mx);
+    CK(hipMemset(out, 0, (size_t)n * m * 8));
+  };
+#define OC(EX, UNR, ROWS, NAME)                                                                    \
+  time([&] { hipLaunchKernelGGL((gram_one_col<D, EX, UNR, ROWS>), dim3((n / ROWS) * (m / GR_COLS)), \
+                                dim3(256), 0, 0, v); }, NAME);                                     \
+  check(NAME);
+  OC(false, 1, 128, "one col, unroll 1, 128 rows")
+  OC(false, 2, 128, "one col, unroll 2, 128 rows")
+  OC(false, 4, 128, "one col, unroll 4, 128 rows")
+  OC(false, 2, 256, "one col, unroll 2, 256 rows")
+  OC(false, 2, 64, "one col, unroll 2, 64 rows")
+  OC(true, 2, 128, "one col, expansion, unroll 2")
+#undef OC
+  CK(hipFree(X)); CK(hipFree(Zp)); CK(hipFree(ref)); CK(hipFree(out)); CK(hipFree(md));
+}
+
+int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IONBF, 0);
+  if (argc > 1 && !strcmp(argv[1], "cols")) {
+    col_study<16>(100096, 4096);
+    col_study<8>(5120, 20096);
+    return 0;
+  }
   const int d = 8, n = 20096, nt = 5120;  // padded C3 sizes (all tiles interior for K*f)
   std::mt19937_64 rng(3);
   std::normal_distribution<double> nd;
