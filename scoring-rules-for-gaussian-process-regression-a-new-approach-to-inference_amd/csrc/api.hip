@@ -160,10 +160,11 @@ struct gps_ctx {
   DBuf fgv, fgm, fgB, fR, fgred, fgslab, fgout;  // FITC gradient scratch
   // block-LOO scratch (per fold, reused): P, its L⁻¹ / P⁻¹ / H, vectors; full-GP Gblk, T;
   // FITC gradient: the fold's G_f, E_f, G_fE_f and F = Gblk E; energy score: work area, draws
-  DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bG, bEf, bFf, bF, ebuf, edraws;
+  DBuf bP, bL, bPI, bH, bvec, bGblk, bT, bkr, bEf, bF, ebuf, edraws;
   // FITC block-LOO fold covariances (fitc_fold_cov): the folds' K_gᵀΛ_g⁻¹K_g slabs, B_{−f} and its
   // L⁻¹ / log-diagonal, the remote ranks' sum, W_f = K_f L_{−f}⁻ᵀ, the fold's padded 1/λ
   DBuf bSg, bBf, bLf, bldf, bRem, bW, bkv;
+  DBuf bLR, bLRv;                      // FITC block-LOO in low rank: b×m products, fold vectors
   DBuf ebuf_aux[3], bPIs, bRW;  // concurrent ES folds: work areas of the aux streams, C_f, r_f / w_f
   DBuf escale;                  // ES: per fold ‖C_f‖∞, then the row-sum scratch
   DBuf bfv;                       // sharded FITC block-LOO: row counts, then the fold values
@@ -1108,18 +1109,15 @@ int es_fold(gps_ctx* ctx, hipStream_t s, DBuf& eb, bool conc, const EsArgs& es, 
   return 0;
 }
 
-// cform (FITC, round 5): getP writes the fold covariance C_f = P_f⁻¹ itself (full, padded as
-// diag(C_f, I)) into its P argument — blockloo_folds then passes C_f's buffer as P⁻¹ — and
-// −½log|C_f| into its last argument (the ½log|P_f| slot); no b×b factorisation or inverse.
 template <class GetP, class GDst, class GDone>
 int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective, const double* alpha,
                    const double* y, GetP getP, bool want_grad, GDst gdst, GDone gdone, double* g,
-                   const EsArgs* es, double* vals, bool cform = false) {
+                   const EsArgs* es, double* vals) {
   hipStream_t s = ctx->stream;
   const int nfold = (int)bnd.size() - 1;
   const int64_t bp = bounds_pad(bnd);
   HIPCHK(ensure(ctx, ctx->bP, (size_t)bp * bp * 8));
-  if (!cform && (ctx->bL.cap < (size_t)bp * bp * 8 || !factor_zeroed(ctx, ctx->bL.d(), bp))) {
+  if (ctx->bL.cap < (size_t)bp * bp * 8 || !factor_zeroed(ctx, ctx->bL.d(), bp)) {
     HIPCHK(ensure(ctx, ctx->bL, (size_t)bp * bp * 8));
     HIPCHK(zero_factor(ctx, ctx->bL.d(), bp, s));
   }
@@ -1157,28 +1155,20 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   HIPCHK(hipMemsetAsync(v, 0, (size_t)9 * bp * 8, s));
   for (int f = 0; f < nfold; ++f) {
     const int64_t a = bnd[f], b = bnd[f + 1] - bnd[f];
-    if (cform) {  // C_f straight into the P⁻¹ buffer: r = C_fα_f, c = diag C_f
-      if ((rc = getP(f, a, b, ctx->bPI.d(), bp, fs + 3 * f))) return rc;
-      HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
-      HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
-      HIPCHK(launch_gemv_full(ctx->bPI.d(), bp, af, r, (int)bp, (int)bp, s));
-      HIPCHK(launch_pad_copy(ctx->bPI.d(), bp + 1, c, 1, (int)b, 1, (int)bp, 1, 0, s));
-    } else {
-      if ((rc = getP(f, a, b, ctx->bP.d(), bp, nullptr))) return rc;
-      if ((rc = potrf_inv(ctx, ctx->bP.d(), bp, ctx->bL.d(), ctx->W.d(), ld, (int)b, nullptr)))
-        return rc;
-      HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
-      HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
-      HIPCHK(launch_gemv_lower(ctx->bL.d(), bp, af, t, (int)bp, s));
-      HIPCHK(launch_colred(ctx->bL.d(), bp, (int)bp, (int)bp, 1, t, nullptr, r, c, ctx->slab.d(), s));
-      HIPCHK(launch_dot(ld, nullptr, (int)b, fs + 3 * f, s));
-    }
+    if ((rc = getP(f, a, b, ctx->bP.d(), bp))) return rc;
+    if ((rc = potrf_inv(ctx, ctx->bP.d(), bp, ctx->bL.d(), ctx->W.d(), ld, (int)b, nullptr)))
+      return rc;
+    HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
+    HIPCHK(launch_pad_copy(y + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
+    HIPCHK(launch_gemv_lower(ctx->bL.d(), bp, af, t, (int)bp, s));
+    HIPCHK(launch_colred(ctx->bL.d(), bp, (int)bp, (int)bp, 1, t, nullptr, r, c, ctx->slab.d(), s));
+    HIPCHK(launch_dot(ld, nullptr, (int)b, fs + 3 * f, s));
     HIPCHK(launch_dot(af, r, (int)b, fs + 3 * f + 1, s));
     if (kc)
       HIPCHK(launch_fold_terms(yf, r, c, (int)b, want_grad ? gm : nullptr, gc, fs + 3 * f + 2, s));
     if (!want_grad && !esq) continue;
     double* PI = es_conc ? PIs + (int64_t)f * bp * bp : ctx->bPI.d();
-    if (!cform) {  // C_f = P⁻¹ = Lp⁻ᵀLp⁻¹ (full)
+    {  // C_f = P⁻¹ = Lp⁻ᵀLp⁻¹ (full)
       GemmParams p = gp0();
       p.A = ctx->bL.d(); p.lda = bp; p.B = ctx->bL.d(); p.ldb = bp; p.C = PI; p.ldc = bp;
       p.M = (int)bp; p.N = (int)bp; p.K = (int)bp; p.tri = TRI_K_GE_I; p.lower_out = 1;
@@ -1269,6 +1259,106 @@ int blockloo_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective,
   return 0;
 }
 
+
+// FITC block-LOO folds in low rank (round 5).  With W = K_f L_{−f}⁻ᵀ (b × m, getW) the fold
+// covariance is C_f = Λ_f + WWᵀ and no b×b matrix is formed: r = C_fα_f = λα + W(Wᵀα),
+// c = diag C_f = λ + ‖W_i‖², and for the gradient F̃_f = G_fŨ_f with
+//   DSS: G_f = −½(C_f + rrᵀ):   F̃ = −½(C_fŨ + r(rᵀŨ)),   diag G = −½(c + r²),   g_f = r
+//   KC:  G_f = ½(wrᵀ + rwᵀ) − C_fDC_f (w = C_f gm, D = diag gc):
+//        F̃ = ½(w(rᵀŨ) + r(wᵀŨ)) − C_f(D·C_fŨ),  C_fX = λX + W(WᵀX),
+//        diag G = w∘r − (λ²gc + 2λ·gc·(c − λ) + rowdot(W(WᵀDW), W)),   g_f = −w
+// (oracle.fast_fitc_blockloo forms the same G_f densely).  Per fold O(b·m²) — 2 (DSS) or 5 (KC)
+// b×m×m products — instead of the b²m covariance and, for KC, the b³ product C_fDC_f.
+template <class GetW>
+int fitc_lr_folds(gps_ctx* ctx, const std::vector<int64_t>& bnd, int objective, const double* alpha,
+                  GetW getW, const double* U, int64_t ldr, double* F, double* gd, double* g,
+                  double* vals) {
+  hipStream_t s = ctx->stream;
+  const int nfold = (int)bnd.size() - 1;
+  const int64_t bp = bounds_pad(bnd), mp = ctx->m_pad;
+  const bool kc = objective == GPS_BLOCK_KC, want = F != nullptr;
+  const int64_t nch = (bp + 255) / 256;
+  HIPCHK(ensure(ctx, ctx->bLRv, (size_t)(10 * bp + 4 * mp + 2 * nch * mp + 3 * nfold + 8) * 8));
+  if (want) HIPCHK(ensure(ctx, ctx->bLR, (size_t)(3 * bp * mp + 2 * mp * mp) * 8));
+  double* lv = ctx->bLRv.d();
+  double *af = lv, *yf = lv + bp, *r = lv + 2 * bp, *c = lv + 3 * bp, *gm = lv + 4 * bp,
+         *gc = lv + 5 * bp, *w = lv + 6 * bp, *at = lv + 7 * bp, *ab = lv + 8 * bp, *q = lv + 9 * bp;
+  double *ta = lv + 10 * bp, *tg = ta + mp, *ru = tg + mp, *wu = ru + mp;
+  double* slab = wu + mp;
+  double* fs = slab + 2 * nch * mp;  // per fold: [−½log|C_f|, α·r, kc]
+  HIPCHK(hipMemsetAsync(lv, 0, (size_t)10 * bp * 8, s));
+  HIPCHK(hipMemsetAsync(fs, 0, (size_t)3 * nfold * 8, s));
+  double* Wf = ctx->bW.d();
+  double *X1 = nullptr, *X2 = nullptr, *X3 = nullptr, *P1 = nullptr, *P2 = nullptr;
+  if (want) {
+    X1 = ctx->bLR.d(); X2 = X1 + bp * mp; X3 = X2 + bp * mp; P1 = X3 + bp * mp; P2 = P1 + mp * mp;
+  }
+  // products with W: Wᵀ X (m × m, K = bp) and W P (bp × m, K = m)
+  auto wt_x = [&](const double* X, double* P, const double* kscale, bool sym) -> int {
+    GemmParams p = gp0();
+    p.A = Wf; p.lda = mp; p.B = X; p.ldb = mp; p.C = P; p.ldc = mp;
+    p.M = (int)mp; p.N = (int)mp; p.K = (int)bp; p.kscale = kscale;
+    if (sym) { p.lower_out = 1; p.mirror = 1; }
+    return gemm(ctx, LAY_T, LAY_N, EPI_STORE, p);
+  };
+  auto w_p = [&](const double* P, double* X) -> int {
+    GemmParams p = gp0();
+    p.A = Wf; p.lda = mp; p.B = P; p.ldb = mp; p.C = X; p.ldc = mp;
+    p.M = (int)bp; p.N = (int)mp; p.K = (int)mp;
+    return gemm(ctx, LAY_N, LAY_N, EPI_STORE, p);
+  };
+  int rc;
+  for (int f = 0; f < nfold; ++f) {
+    const int64_t a = bnd[f], b = bnd[f + 1] - bnd[f];
+    const double* lam = ctx->lam.d() + a;
+    if ((rc = getW(f, a, b, bp, fs + 3 * f))) return rc;
+    HIPCHK(launch_pad_copy(alpha + a, 1, af, 1, (int)b, 1, (int)bp, 1, 0, s));
+    HIPCHK(launch_pad_copy(ctx->fy.d() + a, 1, yf, 1, (int)b, 1, (int)bp, 1, 0, s));
+    HIPCHK(launch_colred(Wf, mp, (int)bp, (int)mp, 0, af, nullptr, ta, nullptr, slab, s));
+    HIPCHK(launch_row_dots(Wf, mp, Wf, mp, ta, (int)bp, (int)mp, at, ab, s));
+    HIPCHK(launch_lr_fold_vec(0, (int)b, (int)bp, lam, af, at, ab, nullptr, nullptr, nullptr,
+                              nullptr, nullptr, r, c, s));
+    HIPCHK(launch_dot(af, r, (int)b, fs + 3 * f + 1, s));
+    if (kc) HIPCHK(launch_fold_terms(yf, r, c, (int)b, want ? gm : nullptr, gc, fs + 3 * f + 2, s));
+    if (!want) continue;
+    double* Uf = ctx->bEf.d();
+    HIPCHK(launch_pad_copy(U + a * ldr, ldr, Uf, mp, (int)b, (int)mp, (int)bp, (int)mp, 0, s));
+    if ((rc = wt_x(Uf, P1, nullptr, false)) || (rc = w_p(P1, X1))) return rc;  // X1 = W(WᵀŨ)
+    HIPCHK(launch_colred(Uf, mp, (int)bp, (int)mp, 0, r, nullptr, ru, nullptr, slab, s));
+    double* Fd = F + a * mp;
+    if (!kc) {
+      HIPCHK(launch_lr_combine(X1, mp, Uf, mp, lam, nullptr, -0.5, r, ru, -0.5, nullptr, nullptr,
+                               0.0, (int)b, (int)b, (int)mp, Fd, mp, s));
+      HIPCHK(launch_lr_fold_vec(3, (int)b, (int)b, lam, nullptr, nullptr, nullptr, r, c, nullptr,
+                                nullptr, nullptr, gd + a, g + a, s));
+      continue;
+    }
+    HIPCHK(launch_colred(Wf, mp, (int)bp, (int)mp, 0, gm, nullptr, tg, nullptr, slab, s));
+    HIPCHK(launch_row_dots(Wf, mp, nullptr, 0, tg, (int)bp, (int)mp, at, nullptr, s));
+    HIPCHK(launch_lr_fold_vec(1, (int)b, (int)bp, lam, gm, at, nullptr, nullptr, nullptr, nullptr,
+                              nullptr, nullptr, w, nullptr, s));
+    // X2 = D·C_fŨ, X3 = W(WᵀX2): C_f(D·C_fŨ) = λX2 + X3
+    HIPCHK(launch_lr_combine(X1, mp, Uf, mp, lam, gc, 1.0, nullptr, nullptr, 0.0, nullptr, nullptr,
+                             0.0, (int)b, (int)bp, (int)mp, X2, mp, s));
+    if ((rc = wt_x(X2, P2, nullptr, false)) || (rc = w_p(P2, X3))) return rc;
+    HIPCHK(launch_colred(Uf, mp, (int)bp, (int)mp, 0, w, nullptr, wu, nullptr, slab, s));
+    HIPCHK(launch_lr_combine(X3, mp, X2, mp, lam, nullptr, -1.0, w, ru, 0.5, r, wu, 0.5, (int)b,
+                             (int)b, (int)mp, Fd, mp, s));
+    // diag(C_fDC_f)'s cross term: rowdot(W(WᵀDW), W)
+    if ((rc = wt_x(Wf, P1, gc, true)) || (rc = w_p(P1, X1))) return rc;
+    HIPCHK(launch_row_dots(X1, mp, Wf, mp, nullptr, (int)bp, (int)mp, nullptr, q, s));
+    HIPCHK(launch_lr_fold_vec(2, (int)b, (int)b, lam, nullptr, nullptr, nullptr, r, c, w, gc, q,
+                              gd + a, g + a, s));
+  }
+  std::vector<double> h((size_t)3 * nfold);
+  HIPCHK(hipMemcpyAsync(h.data(), fs, h.size() * 8, hipMemcpyDeviceToHost, s));
+  if ((rc = check_info(ctx))) return rc;
+  for (int f = 0; f < nfold; ++f) {
+    const double b = (double)(bnd[f + 1] - bnd[f]);
+    vals[f] = kc ? h[3 * f + 2] : 0.5 * b * 1.83787706640934548356 - h[3 * f] + 0.5 * h[3 * f + 1];
+  }
+  return 0;
+}
 }  // namespace
 
 // =============================================================================
@@ -1286,8 +1376,9 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->gu, &ctx->gct, &ctx->gv, &ctx->Mx, &ctx->gslab, &ctx->gout, &ctx->fgv,
                  &ctx->fgm, &ctx->fgB, &ctx->fR, &ctx->fgred, &ctx->fgslab, &ctx->fgout, &ctx->bP,
                  &ctx->bL, &ctx->bPI, &ctx->bH, &ctx->bvec, &ctx->bGblk, &ctx->bT, &ctx->bkr,
-                 &ctx->bG, &ctx->bEf, &ctx->bFf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
+                 &ctx->bEf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
                  &ctx->bSg, &ctx->bBf, &ctx->bLf, &ctx->bldf, &ctx->bRem, &ctx->bW, &ctx->bkv,
+                 &ctx->bLR, &ctx->bLRv,
                  &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->escale, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt};
 }
 
@@ -2600,7 +2691,7 @@ static int full_blockloo(gps_ctx* ctx, int kind, const double* theta, int n_ell,
     HIPCHK(launch_sym_mirror(ctx->A.d(), np, (int)np, s));
   }
   double* Ainv = ctx->A.d();
-  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bp, double*) -> int {
+  auto getP = [&](int, int64_t a, int64_t b, double* P, int64_t bp) -> int {
     HIPCHK(launch_pad_copy(Ainv + a * np + a, np, P, bp, (int)b, (int)b, (int)bp, (int)bp, 1, s));
     return 0;
   };
@@ -2876,9 +2967,6 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     Sm = Bb; T1 = Bb + mp * mp; Sfin = Bb + 2 * mp * mp; KmD = Bb + 3 * mp * mp;
     HIPCHK(ensure(ctx, ctx->bF, (size_t)np * mp * 8));
     HIPCHK(ensure(ctx, ctx->bEf, (size_t)bp * mp * 8));
-    HIPCHK(ensure(ctx, ctx->bFf, (size_t)bp * mp * 8));
-    HIPCHK(ensure(ctx, ctx->bG, (size_t)bp * bp * 8));
-    HIPCHK(hipMemsetAsync(ctx->bG.p, 0, (size_t)bp * bp * 8, s));
     F = ctx->bF.d();
     HIPCHK(hipMemsetAsync(F, 0, (size_t)np * mp * 8, s));
     HIPCHK(hipMemsetAsync(gg, 0, (size_t)2 * np * 8, s));  // g and diag(Gblk)
@@ -2918,45 +3006,24 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     HIPCHK(launch_fold_sum(ctx->bSg.d(), mm, nfl, -1, ctx->bRem.d(), nullptr, -1.0, ctx->bRem.d(), mm, s));
     remote = ctx->bRem.d();
   }
-  auto getP = [&](int fl, int64_t a, int64_t b, double* C, int64_t bpp, double* hl) -> int {
+  // W_f = K_f L_{−f}⁻ᵀ into bW (bpp × mp) and −½log|C_f| (determinant lemma) into *hl
+  auto getW = [&](int fl, int64_t a, int64_t b, int64_t bpp, double* hl) -> int {
     HIPCHK(launch_fold_sum(ctx->bSg.d(), mm, nfl, fl, ctx->Kmm.d(), remote, 1.0, ctx->bBf.d(), mm, s));
     if (int rc2 = potrf_inv(ctx, ctx->bBf.d(), mp, ctx->bLf.d(), ctx->W.d(), ctx->bldf.d(), (int)m,
                             nullptr))
       return rc2;
     HIPCHK(launch_pad_copy(ctx->Knm.d() + a * mp, mp, ctx->bT.d(), mp, (int)b, (int)mp, (int)bpp,
                            (int)mp, 0, s));
-    {  // W_f = K_f L_{−f}⁻ᵀ
-      GemmParams p = gp0();
-      p.A = ctx->bT.d(); p.lda = mp; p.B = ctx->bLf.d(); p.ldb = mp; p.C = ctx->bW.d(); p.ldc = mp;
-      p.M = (int)bpp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
-      if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
-    }
-    {  // C_f = W_f W_fᵀ (full) + Λ_f, padded as diag(C_f, I)
-      GemmParams p = gp0();
-      p.A = ctx->bW.d(); p.lda = mp; p.B = ctx->bW.d(); p.ldb = mp; p.C = C; p.ldc = bpp;
-      p.M = (int)bpp; p.N = (int)bpp; p.K = (int)mp; p.lower_out = 1; p.mirror = 1;
-      if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
-    }
-    HIPCHK(launch_add_diag(C, bpp, ctx->lam.d() + a, (int)b, (int)bpp, s));
+    GemmParams p = gp0();
+    p.A = ctx->bT.d(); p.lda = mp; p.B = ctx->bLf.d(); p.ldb = mp; p.C = ctx->bW.d(); p.ldc = mp;
+    p.M = (int)bpp; p.N = (int)mp; p.K = (int)mp; p.tri = TRI_K_LE_J;
+    if (int rc2 = gemm(ctx, LAY_N, LAY_T, EPI_STORE, p)) return rc2;
     HIPCHK(launch_fold_logdet(ctx->bldf.d(), ctx->ldb.d(), (int)m, ctx->lam.d() + a, (int)b, hl, s));
     return 0;
   };
-  auto gdst = [&](int64_t, int64_t) { return std::make_pair(ctx->bG.d(), bp); };
-  auto gdone = [&](int, int64_t a, int64_t b) -> int {  // F̃ rows of the fold = G_f Ũ_f; diag G_f
-    double* Uf = ctx->bEf.d();
-    double* Ff = ctx->bFf.d();
-    HIPCHK(launch_pad_copy(U + a * ldr, ldr, Uf, mp, (int)b, (int)mp, (int)bp, (int)mp, 0, s));
-    GemmParams p = gp0();
-    p.A = ctx->bG.d(); p.lda = bp; p.B = Uf; p.ldb = mp; p.C = Ff; p.ldc = mp;
-    p.M = (int)bp; p.N = (int)mp; p.K = (int)bp;
-    if (int rc2 = gemm(ctx, LAY_N, LAY_N, EPI_STORE, p)) return rc2;
-    HIPCHK(launch_pad_copy(Ff, mp, F + a * mp, mp, (int)b, (int)mp, (int)b, (int)mp, 0, s));
-    HIPCHK(launch_pad_copy(ctx->bG.d(), bp + 1, gd + a, 1, (int)b, 1, (int)b, 1, 0, s));
-    return 0;
-  };
   std::vector<double> fvl(fid.size()), fv((size_t)nfold, 0.0);
-  if ((rc = blockloo_folds(ctx, bnd, objective, alpha, ctx->fy.d(), getP, want, gdst, gdone,
-                           want ? gg : nullptr, nullptr, fvl.data(), true)))
+  if ((rc = fitc_lr_folds(ctx, bnd, objective, alpha, getW, U, ldr, want ? F : nullptr,
+                          want ? gd : nullptr, want ? gg : nullptr, fvl.data())))
     return rc;
   for (size_t j = 0; j < fid.size(); ++j) fv[fid[j]] = fvl[j];
   if (shard) {  // every fold's value on every rank (each fold is computed by exactly one rank)

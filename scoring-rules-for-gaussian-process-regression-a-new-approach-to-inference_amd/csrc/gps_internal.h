@@ -378,6 +378,20 @@ hipError_t launch_vec_mul(const double* a, const double* b, int n, double* out, 
 hipError_t launch_fold_sum(const double* slab, int64_t stride, int nslab, int skip, const double* base,
                            const double* base2, double sgn, double* dst, int64_t len, hipStream_t s);
 // *out = Σ ldf[<m] − Σ ldb[<m] − ½Σ log lam[<b]: −½log|C_f| of a FITC block-LOO fold covariance
+// FITC block-LOO in low rank (kernels_block.hip): per-row dots of a b×m W, the fold vectors, and
+// the F̃ rows as a base product plus rank-one terms
+hipError_t launch_row_dots(const double* A, int64_t lda, const double* B, int64_t ldb,
+                           const double* t, int rows, int cols, double* at, double* ab,
+                           hipStream_t s);
+hipError_t launch_lr_fold_vec(int mode, int b, int bp, const double* lam, const double* x,
+                              const double* at, const double* ab, const double* r, const double* c,
+                              const double* w, const double* gc, const double* q, double* o1,
+                              double* o2, hipStream_t s);
+hipError_t launch_lr_combine(const double* X, int64_t ldx, const double* Y, int64_t ldy,
+                             const double* lam, const double* rs, double c0, const double* u1,
+                             const double* v1, double c1, const double* u2, const double* v2,
+                             double c2, int rows, int rows_pad, int cols, double* out, int64_t ldo,
+                             hipStream_t s);
 hipError_t launch_fold_logdet(const double* ldf, const double* ldb, int m, const double* lam, int b,
                               double* out, hipStream_t s);
 // FITC block-LOO gradient (whitened): M_ii, the V Lm⁻¹ row scale and Y = −2Λ⁻¹F̃ + 2ŨS̃

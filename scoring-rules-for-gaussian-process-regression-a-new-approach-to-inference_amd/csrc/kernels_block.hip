@@ -72,6 +72,136 @@ hipError_t launch_fold_grad(const double* PI, int64_t ldp, const double* H, int6
   return hipGetLastError();
 }
 
+// ---- FITC block-LOO in low rank (round 5): C_f = Λ_f + W Wᵀ with W = K_f L_{−f}⁻ᵀ (b × m) is
+// never formed; every fold quantity comes from products with W (api.hip fitc_lr_folds).
+
+// one wave per row i < rows: at[i] = Σ_k A[i][k]·t[k] (t != null), ab[i] = Σ_k A[i][k]·B[i][k]
+// (B != null; B = A gives the row norms).  Lane order fixed: bitwise reproducible.
+__global__ __launch_bounds__(256) void row_dots_kernel(const double* __restrict__ A, int64_t lda,
+                                                       const double* __restrict__ B, int64_t ldb,
+                                                       const double* __restrict__ t, int rows,
+                                                       int cols, double* __restrict__ at,
+                                                       double* __restrict__ ab) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const double* a = A + (int64_t)row * lda;
+  const double* bb = B ? B + (int64_t)row * ldb : nullptr;
+  double s1 = 0.0, s2 = 0.0;
+  for (int k = 2 * lane; k < cols; k += 128) {
+    const double2 av = *reinterpret_cast<const double2*>(a + k);
+    if (t) {
+      const double2 tv = *reinterpret_cast<const double2*>(t + k);
+      s1 = fma(av.x, tv.x, s1);
+      s1 = fma(av.y, tv.y, s1);
+    }
+    if (bb) {
+      const double2 bv = *reinterpret_cast<const double2*>(bb + k);
+      s2 = fma(av.x, bv.x, s2);
+      s2 = fma(av.y, bv.y, s2);
+    }
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    if (t) at[row] = s1;
+    if (bb) ab[row] = s2;
+  }
+}
+
+hipError_t launch_row_dots(const double* A, int64_t lda, const double* B, int64_t ldb,
+                           const double* t, int rows, int cols, double* at, double* ab,
+                           hipStream_t s) {
+  if ((cols & 1) || (lda & 1) || (B && (ldb & 1)) || rows <= 0) return rows == 0 ? hipSuccess : hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_dots_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, A, lda, B,
+                     ldb, t, rows, cols, at, ab);
+  return hipGetLastError();
+}
+
+// the per-row fold vectors, i < bp (rows b..bp-1 get 0):
+//   mode 0: o1 = r = λx + at, o2 = c = λ + ab                      (x = α_f)
+//   mode 1: o1 = w = λx + at                                       (x = gm)
+//   mode 2 (KC):  o1 = diag G_f = w∘r − (λ²gc + 2λ·gc·(c − λ) + q),  o2 = g_f = −w
+//   mode 3 (DSS): o1 = diag G_f = −½(c + r²),                         o2 = g_f = r
+__global__ __launch_bounds__(256) void lr_fold_vec_kernel(int mode, int b, int bp,
+                                                          const double* __restrict__ lam,
+                                                          const double* __restrict__ x,
+                                                          const double* __restrict__ at,
+                                                          const double* __restrict__ ab,
+                                                          const double* __restrict__ r,
+                                                          const double* __restrict__ c,
+                                                          const double* __restrict__ w,
+                                                          const double* __restrict__ gc,
+                                                          const double* __restrict__ q,
+                                                          double* __restrict__ o1,
+                                                          double* __restrict__ o2) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= bp) return;
+  if (i >= b) {
+    o1[i] = 0.0;
+    if (o2) o2[i] = 0.0;
+    return;
+  }
+  const double l = lam[i];
+  switch (mode) {
+    case 0: o1[i] = fma(l, x[i], at[i]); o2[i] = l + ab[i]; break;
+    case 1: o1[i] = fma(l, x[i], at[i]); break;
+    case 2: {
+      const double g = gc[i];
+      o1[i] = w[i] * r[i] - (l * l * g + 2.0 * l * g * (c[i] - l) + q[i]);
+      o2[i] = -w[i];
+      break;
+    }
+    default: o1[i] = -0.5 * (c[i] + r[i] * r[i]); o2[i] = r[i]; break;
+  }
+}
+
+hipError_t launch_lr_fold_vec(int mode, int b, int bp, const double* lam, const double* x,
+                              const double* at, const double* ab, const double* r, const double* c,
+                              const double* w, const double* gc, const double* q, double* o1,
+                              double* o2, hipStream_t s) {
+  if (bp <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lr_fold_vec_kernel, dim3((unsigned)((bp + 255) / 256)), dim3(256), 0, s, mode,
+                     b, bp, lam, x, at, ab, r, c, w, gc, q, o1, o2);
+  return hipGetLastError();
+}
+
+// out[i][j] = rs_i·c0·(X[i][j] + λ_i·Y[i][j]) + c1·u1_i·v1_j + c2·u2_i·v2_j for i < rows (rs, the
+// rank-one terms optional), 0 for rows ≤ i < rows_pad; j < cols
+__global__ __launch_bounds__(256) void lr_combine_kernel(const double* __restrict__ X, int64_t ldx,
+                                                         const double* __restrict__ Y, int64_t ldy,
+                                                         const double* __restrict__ lam,
+                                                         const double* __restrict__ rs, double c0,
+                                                         const double* __restrict__ u1,
+                                                         const double* __restrict__ v1, double c1,
+                                                         const double* __restrict__ u2,
+                                                         const double* __restrict__ v2, double c2,
+                                                         int rows, int rows_pad, int cols,
+                                                         double* __restrict__ out, int64_t ldo) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)rows_pad * cols) return;
+  const int i = (int)(e / cols), j = (int)(e - (int64_t)i * cols);
+  double v = 0.0;
+  if (i < rows) {
+    v = c0 * fma(lam[i], Y[(int64_t)i * ldy + j], X[(int64_t)i * ldx + j]);
+    if (rs) v *= rs[i];
+    if (u1) v = fma(c1 * u1[i], v1[j], v);
+    if (u2) v = fma(c2 * u2[i], v2[j], v);
+  }
+  out[(int64_t)i * ldo + j] = v;
+}
+
+hipError_t launch_lr_combine(const double* X, int64_t ldx, const double* Y, int64_t ldy,
+                             const double* lam, const double* rs, double c0, const double* u1,
+                             const double* v1, double c1, const double* u2, const double* v2,
+                             double c2, int rows, int rows_pad, int cols, double* out, int64_t ldo,
+                             hipStream_t s) {
+  const int64_t tot = (int64_t)rows_pad * cols;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(lr_combine_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, ldx,
+                     Y, ldy, lam, rs, c0, u1, v1, c1, u2, v2, c2, rows, rows_pad, cols, out, ldo);
+  return hipGetLastError();
+}
+
 // P[i][i] += vals[i] for i < nreal; P[i][i] = 1 for nreal <= i < npad (diag(P, I) embedding)
 __global__ __launch_bounds__(256) void add_diag_kernel(double* __restrict__ P, int64_t ld,
                                                        const double* __restrict__ vals, int nreal,
