@@ -60,8 +60,13 @@ struct Theta {
 
 // In-process stand-in for the RCCL communicator (gps_comm_init_local): nranks contexts of one
 // process, each driven by its own host thread, meet at every all-reduce of the row-sharded
-// FITC path; the partials are summed on the host in rank order and written back.  Same call
-// sites and extents as ncclAllReduce, so the shard bookkeeping is exercised on one GPU.
+// FITC path.  Same call sites, extents and streams as ncclAllReduce.  Contexts on one device
+// (round 5) sum on the device, stream-ordered like RCCL: each rank copies its partial into a
+// group staging buffer on the calling stream and records an event, the ranks meet on the host
+// (no GPU wait), then each rank's stream waits for every rank's event and sums the staging
+// buffers in rank order into its own buffer — so the stream / event ordering of the sharded
+// sequence (the chunked B exchange on the comm stream beside the SYRK) runs as it would over
+// RCCL, without a host synchronisation.  Contexts on different devices sum on the host.
 struct LocalGroup {
   std::mutex mu;
   std::condition_variable cv;
@@ -73,6 +78,22 @@ struct LocalGroup {
   std::vector<std::vector<double>> in;
   std::vector<double> sum;
   std::vector<char> taken;  // ranks held by a live context (a second context may not join as one)
+  // the device path: one device for every member, ≤ kLocalSumMax ranks
+  int device = -1;
+  bool device_ok = true;
+  std::vector<double*> stage;   // per rank, written only by its owner (grown after every reader)
+  std::vector<size_t> stage_cap;
+  std::vector<hipEvent_t> ready, done;  // per rank: partial staged / staging buffers read
+  ~LocalGroup() {
+    for (hipEvent_t e : done)
+      if (e) (void)hipEventSynchronize(e);
+    for (hipEvent_t e : ready)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : done)
+      if (e) (void)hipEventDestroy(e);
+    for (double* p : stage)
+      if (p) (void)hipFree(p);
+  }
 };
 std::mutex g_groups_mu;
 std::map<long long, std::weak_ptr<LocalGroup>> g_groups;
@@ -811,8 +832,36 @@ void leave_local_group(gps_ctx* ctx) {
   ctx->lgroup.reset();
 }
 
+// one host-side rendezvous of the group's ranks (no GPU wait); every rank passes the same count
+int group_barrier(gps_ctx* ctx, LocalGroup& G, size_t count) {
+  std::unique_lock<std::mutex> lk(G.mu);
+  if (G.aborted) return fail(ctx, -3, "local all-reduce: another rank left the group");
+  if (G.arrived == 0) {
+    G.count = count;
+    G.mismatch = false;
+  } else if (G.count != count) {
+    G.mismatch = true;
+  }
+  const uint64_t my = G.gen;
+  if (++G.arrived == G.n) {
+    G.last_mismatch = G.mismatch;
+    G.arrived = 0;
+    ++G.gen;
+    G.cv.notify_all();
+  } else if (!G.cv.wait_for(lk, std::chrono::seconds(60), [&] { return G.gen != my || G.aborted; })) {
+    G.aborted = true;  // (as in the host path below: the whole group fails the same way)
+    G.cv.notify_all();
+    return fail(ctx, -3, "local all-reduce: timed out waiting for the other ranks (group aborted)");
+  } else if (G.gen == my) {
+    return fail(ctx, -3, "local all-reduce: another rank left the group");
+  }
+  if (G.last_mismatch) return fail(ctx, -3, "local all-reduce: ranks passed different element counts");
+  return 0;
+}
+
 // Σ over the ranks of `count` doubles at buf (device, in place, stream s): ncclAllReduce on
-// the RCCL communicator, or the in-process group's host sum; a no-op on one rank.
+// the RCCL communicator, or the in-process group's sum (on the device when every member shares
+// one); a no-op on one rank.
 int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
   if (ctx->comm) {
     NCCLCHK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, ctx->comm, s));
@@ -820,9 +869,37 @@ int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
   }
   if (!ctx->lgroup) return 0;
   LocalGroup& G = *ctx->lgroup;
+  bool on_device;
   {
     std::lock_guard<std::mutex> lk(G.mu);
     if (G.aborted) return fail(ctx, -3, "local all-reduce: another rank left the group");
+    on_device = G.device_ok;
+  }
+  if (on_device) {
+    const int r = ctx->rank;
+    if (G.stage_cap[r] < count) {  // grow: every earlier sum that read the old buffer is done
+      for (int q = 0; q < G.n; ++q) HIPCHK(hipEventSynchronize(G.done[q]));
+      if (G.stage[r]) HIPCHK(hipFree(G.stage[r]));
+      G.stage[r] = nullptr;
+      G.stage_cap[r] = 0;
+      HIPCHK(hipMalloc(&G.stage[r], count * 8));
+      G.stage_cap[r] = count;
+    }
+    // (the previous sums of the other ranks read this rank's staging buffer: wait for them)
+    for (int q = 0; q < G.n; ++q)
+      if (q != r) HIPCHK(hipStreamWaitEvent(s, G.done[q], 0));
+    HIPCHK(hipMemcpyAsync(G.stage[r], buf, count * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipEventRecord(G.ready[r], s));
+    if (int rc = group_barrier(ctx, G, count)) return rc;  // every rank's ready event recorded
+    LocalSumPtrs sp;
+    memset(&sp, 0, sizeof(sp));
+    for (int q = 0; q < G.n; ++q) {
+      sp.p[q] = G.stage[q];
+      if (q != r) HIPCHK(hipStreamWaitEvent(s, G.ready[q], 0));
+    }
+    HIPCHK(launch_local_sum(sp, G.n, (int64_t)count, buf, s));
+    HIPCHK(hipEventRecord(G.done[r], s));
+    return group_barrier(ctx, G, count);  // every rank's done event recorded before the next use
   }
   std::vector<double> mine(count);
   HIPCHK(hipMemcpyAsync(mine.data(), buf, count * 8, hipMemcpyDeviceToHost, s));
@@ -2265,8 +2342,14 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   HIPCHK(ensure(ctx, ctx->lam, np * 8));
   HIPCHK(ensure(ctx, ctx->ilam, np * 8));
   HIPCHK(ensure(ctx, ctx->ys, np * 8));
+  // (a persistent top level has no recursion step to overlap the q / r pre-passes with)
+  const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
+  // the test pre-pass runs, and without the r pre-pass the test rows stack under Knm in the r
+  // pass (below): g and the row-norm partials then span n_pad + n*_pad rows
+  const bool will_pre = pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof;
+  const int64_t ldr = np + (will_pre && !preq ? ctx->fnt_pad : 0);
   HIPCHK(ensure(ctx, ctx->r, np * 8));
-  HIPCHK(ensure(ctx, ctx->g, np * 8));
+  HIPCHK(ensure(ctx, ctx->g, ldr * 8));
   HIPCHK(ensure(ctx, ctx->fmu_loo, np * 8));
   HIPCHK(ensure(ctx, ctx->fvar_loo, np * 8));
   HIPCHK(ensure(ctx, ctx->c, mp * 8));
@@ -2281,7 +2364,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   // (row-norm partials tm·np; column passes' chunk partials: Knm's 256-row chunks, and, after
   //  the r pass's first column tiles (formed during B's factorisation), the m×m pass for c in
   //  32-row chunks)
-  const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * np, nchunk * mp * 2),
+  const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * ldr, nchunk * mp * 2),
                                               tm * np + (mp + 31) / 32 * mp);
   HIPCHK(ensure(ctx, ctx->fslab, (size_t)fslab_len * 8));
   double* red = ctx->red.d();
@@ -2296,8 +2379,6 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                  ctx->Kmm.d(), mp, (int)mp, (int)mp)))
     return rc;
   HIPCHK(hipMemcpyAsync(ctx->Am.p, ctx->Kmm.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
-  // (a persistent top level has no recursion step to overlap the pre-pass with)
-  const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
   // this shard's rows of K(X, Z): with a pre-pass, first on the main stream (the q column tiles
   // [0, n1) then run on aux[0] inside Lm's captured factorisation, as soon as the top-level
   // Lm11⁻¹ is final); without one, on aux[0] beside Lm's factorisation, whose persistent blocks
@@ -2359,8 +2440,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     return rc;
   }
   if (bside) HIPCHK(hipStreamWaitEvent(s, ctx->b_join, 0));
-  if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
-    if ((rc = fitc_test_prepass(ctx))) return rc;
+  if (will_pre && (rc = fitc_test_prepass(ctx))) return rc;
   // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
   if (shard)
     HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
@@ -2385,22 +2465,40 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                          nullptr, ctx->fslab.d() + tm * np, s, 32));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
-  if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
+  // the test rows' q*b_i = ‖Lb⁻¹k*_i‖²: with one persistent block for B (no r pre-pass), the K*m
+  // rows are stacked under Knm in the r pass's launch (one grid of n_pad + n*_pad rows: C4's
+  // training and test norms were two launches sharing the chip); else on aux[0] beside it
+  const bool stack = ctx->f_pre && ldr > np;  // (ldr > np: no r pre-pass, qn1 = 0)
+  const int64_t ntp = ldr - np;
+  if (stack) {
+    HIPCHK(ensure(ctx, ctx->qb, ntp * 8));
+    HIPCHK(hipStreamWaitEvent(s, ctx->pre_join, 0));  // (K*m: built long before, on aux[0])
+  } else if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) {
+    return rc;
+  }
   {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation), and
      // g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d() + qn1 * mp; p.ldb = mp;
-    p.M = (int)np; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
+    p.M = (int)ldr; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
     p.kend = (int)pad_to(m, 16);
-    p.out0 = ctx->fslab.d() + (qn1 / GPS_TILE) * np; p.ld_out = np;
+    p.out0 = ctx->fslab.d() + (qn1 / GPS_TILE) * ldr; p.ld_out = ldr;
     p.w = ctx->c.d(); p.out1 = ctx->g.d();
+    if (stack) {
+      p.A2 = ctx->Ksm.d();
+      p.m_split = (int)np;
+    }
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ_DOT, p))) return rc;
+  }
+  if (stack) {
+    HIPCHK(launch_slab_sum(ctx->fslab.d() + np, ldr, (int)tm, ntp, nullptr, ctx->qb.d(), s));
+    ctx->f_pre_b = true;
   }
   {  // r = Σ of the row-norm partials, fused with the LOO terms
     part = row_part(ctx, np, 2);
     ARGCHK(part != nullptr, "out of device memory");
     Prof pr(ctx, "fitc_loo", 0, 0);
-    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->fslab.d(), np, (int)tm, ctx->g.d(),
+    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->fslab.d(), ldr, (int)tm, ctx->g.d(),
                            (int)n, (int)np, ctx->r.d(), ctx->fmu_loo.d(), ctx->fvar_loo.d(),
                            scal + 2, part, s));
   }
@@ -3334,6 +3432,17 @@ int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
     G->n = nranks;
     G->in.resize(nranks);
     G->taken.assign(nranks, 0);
+    G->device = ctx->device;
+    G->device_ok = nranks <= kLocalSumMax;
+    G->stage.assign(nranks, nullptr);
+    G->stage_cap.assign(nranks, 0);
+    G->ready.assign(nranks, nullptr);
+    G->done.assign(nranks, nullptr);
+    if (G->device_ok)
+      for (int q = 0; q < nranks; ++q) {
+        HIPCHK(hipEventCreateWithFlags(&G->ready[q], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&G->done[q], hipEventDisableTiming));
+      }
     g_groups[group] = G;
   }
   ARGCHK(G->n == nranks, "local group: nranks differs from the group's");
@@ -3341,6 +3450,7 @@ int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
     std::lock_guard<std::mutex> gl(G->mu);
     ARGCHK(!G->taken[rank], "local group: another live context already holds this rank");
     G->taken[rank] = 1;
+    if (ctx->device != G->device) G->device_ok = false;  // members on two devices: host sums
   }
   ctx->lgroup = G;
   ctx->nranks = nranks;

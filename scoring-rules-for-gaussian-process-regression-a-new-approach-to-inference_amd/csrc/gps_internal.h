@@ -66,7 +66,7 @@ struct GemmParams {
   int tiles_m, tiles_n;
   int map_mode;              // tile order: 0 auto (see tile_of), 1 grouped raster only, 2 + XCD remap,
                              // 3 XCD-banded heaviest-first (auto for triangular), 4 pre-3 auto,
-                             // 5 XCD-banded 8×8 patches (auto for EPI_ROWSQ)
+                             // 5 XCD-banded 8×8 patches, 6 paired column tiles (EPI_ROWSQ*)
   int tile;                  // output tile edge: 0 auto (gemm_plan), 64 or 128
   double* ws;                // split-K workspace: slabs + ordered reduction (auto plan only
   int64_t ws_cap;            //   splits while ksplit*M*N <= ws_cap doubles)
@@ -89,6 +89,9 @@ struct GemmParams {
   int sk_alone;              // the launch runs without a concurrent forked product (potrf_inv_rec's
                              // trailing update when nothing is forked beside it): the stream-K
                              // tail fills its last round (GPS_OPT_STREAM_K = 2, the default)
+  const double* A2;          // (row-major A only) rows >= m_split come from A2 (row m_split = A2's
+  int m_split;               // row 0, same lda): two row panels stacked in one launch (the FITC
+                             // training and test row norms over Lb⁻¹); a multiple of 128
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
@@ -378,6 +381,13 @@ hipError_t launch_vec_mul(const double* a, const double* b, int n, double* out, 
 hipError_t launch_fold_sum(const double* slab, int64_t stride, int nslab, int skip, const double* base,
                            const double* base2, double sgn, double* dst, int64_t len, hipStream_t s);
 // *out = Σ ldf[<m] − Σ ldb[<m] − ½Σ log lam[<b]: −½log|C_f| of a FITC block-LOO fold covariance
+// the in-process communicator's device sum (kernels_vec.hip): up to kLocalSumMax ranks' staging
+// buffers summed in rank order
+constexpr int kLocalSumMax = 64;
+struct LocalSumPtrs {
+  const double* p[kLocalSumMax];
+};
+hipError_t launch_local_sum(const LocalSumPtrs& sp, int n, int64_t count, double* out, hipStream_t s);
 // FITC block-LOO in low rank (kernels_block.hip): per-row dots of a b×m W, the fold vectors, and
 // the F̃ rows as a base product plus rank-one terms
 hipError_t launch_row_dots(const double* A, int64_t lda, const double* B, int64_t ldb,

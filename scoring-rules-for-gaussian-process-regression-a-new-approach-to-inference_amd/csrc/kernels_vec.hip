@@ -523,6 +523,24 @@ hipError_t launch_pad_copy(const double* src, int64_t lds, double* dst, int64_t 
   return hipGetLastError();
 }
 
+// in-process all-reduce (api.hip allreduce_sum, local group): out[i] = Σ_q src[q][i] in rank order
+// from 0.0 — the same sum, in the same order, as the group's host path
+__global__ __launch_bounds__(256) void local_sum_kernel(LocalSumPtrs sp, int n, int64_t count,
+                                                        double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  double v = 0.0;
+  for (int q = 0; q < n; ++q) v += sp.p[q][i];
+  out[i] = v;
+}
+hipError_t launch_local_sum(const LocalSumPtrs& sp, int n, int64_t count, double* out, hipStream_t s) {
+  if (n < 1 || n > kLocalSumMax) return hipErrorInvalidValue;
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(local_sum_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, sp, n,
+                     count, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_trmv_lower(const double* L, int64_t ldl, const double* x, double* y, int n_pad,
                              int trans, hipStream_t s) {
   if (!trans) return launch_gemv_lower(L, ldl, x, y, n_pad, s);
