@@ -2342,14 +2342,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   HIPCHK(ensure(ctx, ctx->lam, np * 8));
   HIPCHK(ensure(ctx, ctx->ilam, np * 8));
   HIPCHK(ensure(ctx, ctx->ys, np * 8));
-  // (a persistent top level has no recursion step to overlap the q / r pre-passes with)
-  const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
-  // the test pre-pass runs, and without the r pre-pass the test rows stack under Knm in the r
-  // pass (below): g and the row-norm partials then span n_pad + n*_pad rows
-  const bool will_pre = pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof;
-  const int64_t ldr = np + (will_pre && !preq ? ctx->fnt_pad : 0);
   HIPCHK(ensure(ctx, ctx->r, np * 8));
-  HIPCHK(ensure(ctx, ctx->g, ldr * 8));
+  HIPCHK(ensure(ctx, ctx->g, np * 8));
   HIPCHK(ensure(ctx, ctx->fmu_loo, np * 8));
   HIPCHK(ensure(ctx, ctx->fvar_loo, np * 8));
   HIPCHK(ensure(ctx, ctx->c, mp * 8));
@@ -2364,7 +2358,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   // (row-norm partials tm·np; column passes' chunk partials: Knm's 256-row chunks, and, after
   //  the r pass's first column tiles (formed during B's factorisation), the m×m pass for c in
   //  32-row chunks)
-  const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * ldr, nchunk * mp * 2),
+  const int64_t fslab_len = std::max<int64_t>(std::max<int64_t>(tm * np, nchunk * mp * 2),
                                               tm * np + (mp + 31) / 32 * mp);
   HIPCHK(ensure(ctx, ctx->fslab, (size_t)fslab_len * 8));
   double* red = ctx->red.d();
@@ -2379,6 +2373,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                  ctx->Kmm.d(), mp, (int)mp, (int)mp)))
     return rc;
   HIPCHK(hipMemcpyAsync(ctx->Am.p, ctx->Kmm.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
+  // (a persistent top level has no recursion step to overlap the pre-pass with)
+  const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
   // this shard's rows of K(X, Z): with a pre-pass, first on the main stream (the q column tiles
   // [0, n1) then run on aux[0] inside Lm's captured factorisation, as soon as the top-level
   // Lm11⁻¹ is final); without one, on aux[0] beside Lm's factorisation, whose persistent blocks
@@ -2440,7 +2436,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
     return rc;
   }
   if (bside) HIPCHK(hipStreamWaitEvent(s, ctx->b_join, 0));
-  if (will_pre && (rc = fitc_test_prepass(ctx))) return rc;
+  if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
+    if ((rc = fitc_test_prepass(ctx))) return rc;
   // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
   if (shard)
     HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
@@ -2465,40 +2462,22 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                          nullptr, ctx->fslab.d() + tm * np, s, 32));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
-  // the test rows' q*b_i = ‖Lb⁻¹k*_i‖²: with one persistent block for B (no r pre-pass), the K*m
-  // rows are stacked under Knm in the r pass's launch (one grid of n_pad + n*_pad rows: C4's
-  // training and test norms were two launches sharing the chip); else on aux[0] beside it
-  const bool stack = ctx->f_pre && ldr > np;  // (ldr > np: no r pre-pass, qn1 = 0)
-  const int64_t ntp = ldr - np;
-  if (stack) {
-    HIPCHK(ensure(ctx, ctx->qb, ntp * 8));
-    HIPCHK(hipStreamWaitEvent(s, ctx->pre_join, 0));  // (K*m: built long before, on aux[0])
-  } else if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) {
-    return rc;
-  }
+  if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
   {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation), and
      // g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d() + qn1 * mp; p.ldb = mp;
-    p.M = (int)ldr; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
+    p.M = (int)np; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
     p.kend = (int)pad_to(m, 16);
-    p.out0 = ctx->fslab.d() + (qn1 / GPS_TILE) * ldr; p.ld_out = ldr;
+    p.out0 = ctx->fslab.d() + (qn1 / GPS_TILE) * np; p.ld_out = np;
     p.w = ctx->c.d(); p.out1 = ctx->g.d();
-    if (stack) {
-      p.A2 = ctx->Ksm.d();
-      p.m_split = (int)np;
-    }
     if ((rc = gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ_DOT, p))) return rc;
-  }
-  if (stack) {
-    HIPCHK(launch_slab_sum(ctx->fslab.d() + np, ldr, (int)tm, ntp, nullptr, ctx->qb.d(), s));
-    ctx->f_pre_b = true;
   }
   {  // r = Σ of the row-norm partials, fused with the LOO terms
     part = row_part(ctx, np, 2);
     ARGCHK(part != nullptr, "out of device memory");
     Prof pr(ctx, "fitc_loo", 0, 0);
-    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->fslab.d(), ldr, (int)tm, ctx->g.d(),
+    HIPCHK(launch_fitc_loo(ctx->fy.d(), ctx->lam.d(), ctx->fslab.d(), np, (int)tm, ctx->g.d(),
                            (int)n, (int)np, ctx->r.d(), ctx->fmu_loo.d(), ctx->fvar_loo.d(),
                            scal + 2, part, s));
   }

@@ -89,9 +89,6 @@ struct GemmParams {
   int sk_alone;              // the launch runs without a concurrent forked product (potrf_inv_rec's
                              // trailing update when nothing is forked beside it): the stream-K
                              // tail fills its last round (GPS_OPT_STREAM_K = 2, the default)
-  const double* A2;          // (row-major A only) rows >= m_split come from A2 (row m_split = A2's
-  int m_split;               // row 0, same lda): two row panels stacked in one launch (the FITC
-                             // training and test row norms over Lb⁻¹); a multiple of 128
 };
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark

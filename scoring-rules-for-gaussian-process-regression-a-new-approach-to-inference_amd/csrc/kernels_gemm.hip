@@ -309,8 +309,6 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int row0 = ti * TILE, col0 = tj * TILE;
-  // a stacked second row panel (GemmParams::A2): the tile lies wholly in one of the two
-  const double* Aop = (ALAY == LAY_N && p.A2 && row0 >= p.m_split) ? p.A2 - (int64_t)p.m_split * p.lda : p.A;
 
   int kb = 0, ke = p.K;
   switch (p.tri) {
@@ -352,7 +350,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
       }
     } else {  // A stored [i][k]
       const int i = tid / TPI, k = (tid % TPI) * PER;
-      const dv2* src = reinterpret_cast<const dv2*>(Aop + (int64_t)(row0 + i) * p.lda + k0 + k);
+      const dv2* src = reinterpret_cast<const dv2*>(p.A + (int64_t)(row0 + i) * p.lda + k0 + k);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) ra[q] = src[q];
       if (p.kscale) {
@@ -833,9 +831,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   if ((p.lda & 1) || (p.ldb & 1) || (p.ldc & 1)) return hipErrorInvalidValue;
   if (p.lower_out && p.M != p.N) return hipErrorInvalidValue;
   if (p.mirror && (!p.lower_out || p.M % 32)) return hipErrorInvalidValue;
-  // a stacked row panel: row-major A, 128-tile launches, the split on a tile boundary
-  if (p.A2 && (alay != LAY_N || p.m_split <= 0 || p.m_split % 128 || p.m_split >= p.M))
-    return hipErrorInvalidValue;
   if (p.ksplit < 1) p.ksplit = 1;
   // the row dot comes from the last column tile, which must span the whole K range (columns
   // [tri_off, tri_off + N) of a larger triangular product whose last column is K)
@@ -845,7 +840,6 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
     return hipErrorInvalidValue;
   const GemmPlan plan = gemm_plan(epi, p, p.ws ? p.ws_cap : 0);
   const int tile = plan.tile;
-  if (p.A2 && tile != 64 && tile != 128) return hipErrorInvalidValue;  // (the small kernel: one A)
   if (tile == 16 || tile == 32) {  // small kernel: tile = block edge, ksplit = waves per block
     if (epi != EPI_STORE || p.kscale) return hipErrorInvalidValue;
     const int wpt = plan.ksplit;
