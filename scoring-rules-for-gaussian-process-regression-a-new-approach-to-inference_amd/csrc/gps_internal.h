@@ -81,11 +81,8 @@ struct GemmParams {
                              // reduction when there is one, else by launch_sym_mirror)
   int slab_xcd;              // set by launch_gemm (g_slab_xcd): a split-K grid's (tile, slice)
                              // pairs dealt slice-major in contiguous runs per XCD
-  int kend;                  // > 0 (a multiple of 16): A's columns k >= kend are zero and B's rows
-                             // j >= kend its identity padding (the FITC row norms: kend = m rounded
-                             // to 16) — the K loop stops there and, for EPI_ROWSQ*, 16-column
-                             // blocks of such rows (and, TRI_K_LE_J, slices above a block's
-                             // diagonal) skip their MFMAs: exact zeros either way
+  int kend;                  // > 0 (a multiple of 16): A's columns k >= kend are zero (the FITC row
+                             // norms: kend = m rounded to 16) — the K loop stops there
   int sk_alone;              // the launch runs without a concurrent forked product (potrf_inv_rec's
                              // trailing update when nothing is forked beside it): the stream-K
                              // tail fills its last round (GPS_OPT_STREAM_K = 2, the default)

@@ -30,8 +30,6 @@
 // diagonal 128-blocks of a triangular factor are stored with explicit zeros
 // above the diagonal, so clipping at 64 or 128 granularity never drops a
 // nonzero) — no multiply touches a structurally zero tile.
-#include <climits>
-
 #include "gps_internal.h"
 
 namespace gps {
@@ -408,28 +406,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
 #pragma unroll
     for (int ni = 0; ni < MI; ++ni) acc[mi][ni] = (d4){0.0, 0.0, 0.0, 0.0};
 
-  // The FITC row norms (EPI_ROWSQ*, B = rows of a triangular L⁻¹, TRI_K_LE_J): a 16-column block of
-  // B whose rows lie in the identity padding (>= kend) or whose entries in this 16-deep slice are
-  // all above the rows' diagonal contributes exact zeros — its MFMAs are skipped (round 5: 12 % of
-  // the row norms' MFMAs at m = 2000, the m_pad padding and the zero halves of the diagonal blocks)
-  constexpr bool SKIP = EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT;
-  const int gcol = p.tri_off + col0 + wc * WT;  // global B row of the wave's first column block
-  const int kend_b = p.kend > 0 ? p.kend : INT_MAX;
-  auto active = [&](int k0) -> unsigned {
-    if constexpr (!SKIP) {
-      return (1u << MI) - 1;
-    } else {
-      unsigned m = 0;
-#pragma unroll
-      for (int ni = 0; ni < MI; ++ni) {
-        const int c = gcol + 16 * ni;
-        const bool on = c < kend_b && (p.tri != TRI_K_LE_J || k0 < c + 16);
-        m |= on ? 1u << ni : 0u;
-      }
-      return __builtin_amdgcn_readfirstlane(m);
-    }
-  };
-  auto compute = [&](int buf, unsigned act) {
+  auto compute = [&](int buf) {
     const double* As = smem + buf * STAGE;
     const double* Bs = As + BK * LS;
 #pragma unroll
@@ -444,8 +421,7 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < MI; ++ni)
-          if (act >> ni & 1)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
     }
   };
 
@@ -473,13 +449,13 @@ __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, i
     for (int it = 0; it < nk - 1; ++it) {
       load_tile(kb + (it + 1) * BK);
       if (p.prio) __builtin_amdgcn_s_setprio(1);
-      compute(it & 1, active(kb + it * BK));
+      compute(it & 1);
       if (p.prio) __builtin_amdgcn_s_setprio(0);
       row_dot(it & 1, kb + it * BK);
       store_tile((it + 1) & 1);
       __syncthreads();
     }
-    compute((nk - 1) & 1, active(kb + (nk - 1) * BK));
+    compute((nk - 1) & 1);
     row_dot((nk - 1) & 1, kb + (nk - 1) * BK);
   }
   if constexpr (EPI == EPI_ROWSQ_DOT) {
