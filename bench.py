@@ -914,12 +914,14 @@ def main():
                     fgstep()
                     k = max(1, args.steps // 2)
                     fg[objective] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, fgstep, k) / k}
-                if leg == "C4" and world == 1 and not args.no_block:  # next-2: K20:655-726 KC
-                    def fbstep():
-                        return fgp.block_loo(thf, "kc", grad=True)
-                    fbstep()
-                    fg["block_kc"] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, fbstep, 1),
-                                      "note": "4 folds of 10 000 rows, theta and Z gradient"}
+                if leg == "C4" and world == 1 and not args.no_block:  # next-2: K20:655-726 KC,
+                    for bobj in ("kc", "dss"):                        # K20:523-587 DSS
+                        def fbstep():
+                            return fgp.block_loo(thf, bobj, grad=True)
+                        fbstep()
+                        fg["block_" + bobj] = {"ms_per_iteration": 1e3 * timed(ctl, ctx, fbstep, 1),
+                                               "note": "4 folds of 10 000 rows, theta and Z gradient "
+                                                       "(folds in low rank, DESIGN.md §10)"}
                 fitc[leg]["grad"] = fg
             del Xf, yf, Xtf, ytf
         if world > 1 and not args.rehearse and "error" not in fitc:

@@ -266,7 +266,10 @@ static int rowsq_study(double* A, double* B, double* o0) {
 // where the row norms lose against the square products: the C4 fit shape as row norms and as a
 // stored product, triangular K and full K, against the square 10k shape in both epilogues
 static int rowsq_iso(double* A, double* B, double* C, double* o0) {
-  struct S { const char* name; int M, N, epi, tri, mm; } cs[] = {
+  struct S { const char* name; int M, N, epi, tri, mm, K = 0; } cs[] = {
+    {"C4fit rowsq full K=1024", 40064, 2048, EPI_ROWSQ, TRI_NONE, 0, 1024},
+    {"C4fit rowsq full K=512", 40064, 2048, EPI_ROWSQ, TRI_NONE, 0, 512},
+    {"C4fit store full K=1024", 40064, 2048, EPI_STORE, TRI_NONE, 0, 1024},
     {"C4fit rowsq tri map5", 40064, 2048, EPI_ROWSQ, TRI_K_LE_J, 0},
     {"C4fit rowsq tri map3", 40064, 2048, EPI_ROWSQ, TRI_K_LE_J, 3},
     {"C4fit rowsq tri map6", 40064, 2048, EPI_ROWSQ, TRI_K_LE_J, 6},
@@ -292,10 +295,11 @@ static int rowsq_iso(double* A, double* B, double* C, double* o0) {
       const S& c = cs[pass == 1 ? nc - 1 - ci : ci];
       memset(&p, 0, sizeof(p));
       p.A = A; p.B = B; p.C = C; p.out0 = o0; p.alpha = 1.0; p.ksplit = 1; p.tile = 0;
-      p.lda = c.N; p.ldb = c.N; p.ldc = c.N; p.ld_out = c.M;
-      p.M = c.M; p.N = c.N; p.K = c.N; p.tri = c.tri; p.map_mode = c.mm;
+      const int K = c.K ? c.K : c.N;
+      p.lda = K; p.ldb = K; p.ldc = c.N; p.ld_out = c.M;
+      p.M = c.M; p.N = c.N; p.K = K; p.tri = c.tri; p.map_mode = c.mm;
       g_gemm_prio = prio ? 2 : 0;
-      const double fl = (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)c.N;
+      const double fl = (c.tri ? 1.0 : 2.0) * c.M * c.N * (double)K;
       printf("p%d %-24s prio%d %7.2f TF/s\n", pass, c.name, prio, run(LAY_N, LAY_T, c.epi, p, 5, fl));
     }
   g_gemm_prio = 1;
