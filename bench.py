@@ -78,7 +78,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, one_gpu_rccl=False):
     """`bench.py --gpus N` without a launcher's WORLD_SIZE: start N rank processes of this same
     script (one per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free
     MASTER_PORT) and wait on them.  This parent only spawns and collects: it never imports torch or
@@ -98,6 +98,8 @@ def spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
                    MASTER_PORT=port)
+        if one_gpu_rccl:  # (--one-gpu-rccl: each rank its own RCCL host id, loopback sockets)
+            env.update(NCCL_HOSTID=f"gpscore-rank-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
     rc = 0
@@ -662,6 +664,12 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 control-plane rehearsal on a 1-GPU box: every rank on device 0, "
                          "no RCCL communicator (FITC objectives then cover the local shard only)")
+    ap.add_argument("--one-gpu-rccl", action="store_true",
+                    help="functional test of the N>1 RCCL path on a 1-GPU box: every rank on device 0 "
+                         "with a REAL RCCL communicator — each rank presents its own NCCL_HOSTID, so "
+                         "RCCL's one-rank-per-GPU check passes and the ranks exchange over loopback "
+                         "sockets; the rank-count and C5-vs-N=1 checks run as at N>1 (not a "
+                         "performance run: the ranks share one GPU)")
     ap.add_argument("--write-c5-fixture", metavar="PATH", default=None,
                     help="N = 1 only: write the C5 unit's rank-independent outputs (fitc_outputs) "
                          "to PATH — the fixture tests/golden/c5_n1_outputs.json that N > 1 runs "
@@ -675,7 +683,7 @@ def main():
         ap.error("--gpus must be >= 1")
     # --gpus N with no launcher around us: this process becomes the spawner, before any GPU call
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, args.one_gpu_rccl))
     world, rank, local = dist_env()
     if world != args.gpus:
         print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a "
@@ -714,7 +722,7 @@ def main():
         return
     import gpscore
     failures = []  # self-checks that fail the run (non-zero exit) after the JSON line
-    ctx = gpscore.Context(0 if args.rehearse else local)
+    ctx = gpscore.Context(0 if (args.rehearse or args.one_gpu_rccl) else local)
     if args.no_tiny_gemm:
         ctx.set_tiny_gemm(False)
     gp = gpscore.GP(ctx=ctx)
@@ -767,7 +775,8 @@ def main():
         "dtype": "f64", "data": "synthetic (SURVEY.md §8d generator; random-init theta fixed)",
         "config": {"workload": f"{args.config} full GP fit(NLML+LOO-CRPS+LOO-LogS)+predict+score",
                    "n": c["n"], "d": c["d"], "n_test": c["nt"], "kernel": "ARD",
-                   "parallelism": "replicas" if world > 1 else "single"},
+                   "parallelism": (("replicas on ONE GPU, RCCL functional test (--one-gpu-rccl)"
+                                    if args.one_gpu_rccl else "replicas") if world > 1 else "single")},
         "roofline": roofline_mfma(prof, traffic, args.steps, alg_flop("full", c)),
         "roofline_gram": roofline_gram(prof, args.steps, traffic_gram),
         "roofline_trailing_update": roofline_trailing(prof, args.steps),

@@ -1,0 +1,55 @@
+"""One rank of tests/test_gpu_rccl.py: a REAL RCCL communicator on a one-GPU box.
+
+Started as its own process by the test (never collected by pytest: no test_ prefix).  Each rank
+presents its own NCCL_HOSTID (set by the parent), so RCCL's one-rank-per-GPU check passes and the
+ranks exchange over the socket transport on loopback; the ranks meet over gloo only to broadcast
+RCCL's unique id.  The rank fits its row shard of the test_gpu_shards case through
+gpscore.dist.attach_comm (gps_comm_init → ncclCommInitRank) and writes its outputs and what the
+communicator reports (gps_comm_info) to <outdir>/rank<r>.npz.
+    argv: outdir n nt m d seed
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [HERE, os.path.join(ROOT, "oracle"), ROOT,
+                os.path.join(ROOT, "scoring-rules-for-gaussian-process-regression-a-new-approach-to-inference_amd")]
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    outdir = sys.argv[1]
+    n, nt, m, d, seed = (int(v) for v in sys.argv[2:7])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gpscore
+    from gpscore.dist import attach_comm, shard_rows
+    from test_gpu_shards import _case, _run
+    X, y, Xt, yt, Z, th = _case(n, nt, m, d, seed)
+    ctx = gpscore.Context(0)
+    gp = gpscore.GP(ctx=ctx)
+    attach_comm(gp)
+    info = ctx.comm_info()
+    a, b = shard_rows(n, world, rank)
+    ta, tb = shard_rows(nt, world, rank)
+    gp.set_data(X[a:b], y[a:b], kind="fitc", Z=Z, n_total=n, ytr_stats=(float(y.mean()), float(y.var(ddof=1))))
+    gp.set_test(Xt[ta:tb], yt[ta:tb], nt_total=nt)
+    res = _run(gp, th, True)
+    out = {"comm": np.array(info[:2], dtype=np.int64), "kind": np.array(info[2]),
+           "obj_keys": np.array(sorted(res["obj"])), "obj": np.array([res["obj"][k] for k in sorted(res["obj"])]),
+           "sc_keys": np.array(sorted(res["sc"])), "sc": np.array([res["sc"][k] for k in sorted(res["sc"])])}
+    for k, v in res.items():
+        if k not in ("obj", "sc"):
+            out[k] = np.asarray(v)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
+    ctx.call("gps_comm_destroy")
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

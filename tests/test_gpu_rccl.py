@@ -1,0 +1,78 @@
+"""The row-sharded FITC path over a REAL RCCL communicator with 2 and 3 ranks, on a one-GPU box
+(K20:222-234, 270-296, 236/344/452).
+
+RCCL refuses two ranks on one device ("Duplicate GPU detected"); each rank process here
+(tests/rccl_rank.py) presents its own NCCL_HOSTID, so the check passes and the ranks exchange
+over the socket transport on loopback instead of xGMI — the same ncclCommInitRank, the same
+ncclAllReduce calls on the same streams in the same order as on an 8-GPU node, only slower
+links.  Each rank reports what its communicator holds (gps_comm_info: RCCL's ncclCommCount /
+ncclCommUserRank), and the gathered shards must match the unsharded fit within 30× the measured
+conditioning floor, as the in-process shards of test_gpu_shards do.
+"""
+import os
+import signal
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from test_gpu_shards import _case, _compare, _floor, _whole
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rccl_ranks(P, outdir, args, timeout=240):
+    port = str(_free_port())
+    procs = []
+    for r in range(P):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(P),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, NCCL_HOSTID=f"gpscore-test-rank-{r}",
+                   NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "rccl_rank.py"), str(outdir)]
+                                      + [str(a) for a in args], env=env, start_new_session=True))
+    codes = []
+    try:
+        for p in procs:
+            codes.append(p.wait(timeout=timeout))
+    finally:
+        for p in procs:  # (a rank left inside a collective: end its whole session)
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    assert codes == [0] * P, codes
+    parts = []
+    for r in range(P):
+        z = np.load(os.path.join(outdir, f"rank{r}.npz"))
+        part = {"comm": z["comm"].tolist(), "kind": str(z["kind"]),
+                "obj": dict(zip(z["obj_keys"].tolist(), z["obj"].tolist())),
+                "sc": dict(zip(z["sc_keys"].tolist(), z["sc"].tolist()))}
+        for k in z.files:
+            if k not in ("comm", "kind", "obj_keys", "obj", "sc_keys", "sc"):
+                part[k] = z[k]
+        parts.append(part)
+    return parts
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_fitc_rccl_ranks_match_unsharded(gpu_ctx, tmp_path, P):
+    """n = 6001 (ragged shards), m = 300, d = 8: forward, predict, scores and the θ / Z gradients
+    of all three objectives over RCCL, each within 30× its measured conditioning floor; every
+    rank's communicator counts P ranks and the user ranks are 0..P−1."""
+    args = (6001, 1501, 300, 8, 41)
+    parts = _rccl_ranks(P, tmp_path, args)
+    for r, p in enumerate(parts):
+        assert p["comm"] == [P, r] and p["kind"] == "rccl", (p["comm"], p["kind"])
+    X, y, Xt, yt, Z, th = _case(*args)
+    ref = _whole(X, y, Xt, yt, Z, th, True, gpu_ctx)
+    from test_gpu_parity import fitc_cap
+    _compare(parts, ref, _floor(X, y, Xt, yt, Z, th, True, gpu_ctx, ref), fitc_cap(Z, th),
+             f"fitc_rccl_P{P}")

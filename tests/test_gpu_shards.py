@@ -2,7 +2,8 @@
 host thread, joined by the in-process communicator (gps_comm_init_local).  Every all-reduce
 of the sharded path — the lower-packed B / b / scalar reduction of the forward, the LOO and
 test-score sums, the four gradient reductions — runs at the same call sites with the same
-element counts as under RCCL, with the partials summed on the host in rank order.  The
+element counts as under RCCL, the partials summed on the device in rank order, stream-ordered
+on the calling streams like ncclAllReduce (round 5; test_gpu_rccl runs a real RCCL communicator).  The
 sharded results must match the unsharded fit (K20:222-234, 270-296, 236/344/452).
 """
 from concurrent.futures import ThreadPoolExecutor
