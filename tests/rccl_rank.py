@@ -6,7 +6,9 @@ ranks exchange over the socket transport on loopback; the ranks meet over gloo o
 RCCL's unique id.  The rank fits its row shard of the test_gpu_shards case through
 gpscore.dist.attach_comm (gps_comm_init → ncclCommInitRank) and writes its outputs and what the
 communicator reports (gps_comm_info) to <outdir>/rank<r>.npz.
-    argv: outdir n nt m d seed
+    argv: outdir n nt m d seed [block nfold objective]
+With `block`, the rows are sharded on fold boundaries (gpscore.dist.fold_shard_rows) and the rank
+writes its block-LOO value, fold values and θ- / Z-gradients instead (K20:523-587, 655-720).
 """
 import os
 import sys
@@ -33,6 +35,21 @@ def main():
     gp = gpscore.GP(ctx=ctx)
     attach_comm(gp)
     info = ctx.comm_info()
+    if len(sys.argv) > 7 and sys.argv[7] == "block":
+        from gpscore.dist import fold_shard_rows
+        nfold, objective = int(sys.argv[8]), sys.argv[9]
+        a, b = fold_shard_rows(n, nfold, world, rank)
+        gp.set_data(X[a:b], y[a:b], kind="fitc", Z=Z, n_total=n,
+                    ytr_stats=(float(y.mean()), float(y.var(ddof=1))))
+        v, g, f, gz = gp.block_loo(th, objective, nfold=nfold, grad=True)
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), comm=np.array(info[:2], dtype=np.int64),
+                 kind=np.array(info[2]), value=np.array(v), folds=np.asarray(f), grad=np.asarray(g),
+                 grad_Z=np.asarray(gz))
+        ctx.call("gps_comm_destroy")
+        ctx.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     a, b = shard_rows(n, world, rank)
     ta, tb = shard_rows(nt, world, rank)
     gp.set_data(X[a:b], y[a:b], kind="fitc", Z=Z, n_total=n, ytr_stats=(float(y.mean()), float(y.var(ddof=1))))

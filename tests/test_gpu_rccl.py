@@ -18,7 +18,7 @@ import sys
 import numpy as np
 import pytest
 
-from test_gpu_shards import _case, _compare, _floor, _whole
+from test_gpu_shards import _blockloo_check, _case, _compare, _floor, _whole
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -30,7 +30,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rccl_ranks(P, outdir, args, timeout=240):
+def _rccl_ranks(P, outdir, args, timeout=240, raw=False):
     port = str(_free_port())
     procs = []
     for r in range(P):
@@ -49,6 +49,8 @@ def _rccl_ranks(P, outdir, args, timeout=240):
                 os.killpg(p.pid, signal.SIGKILL)
                 p.wait()
     assert codes == [0] * P, codes
+    if raw:
+        return [dict(np.load(os.path.join(outdir, f"rank{r}.npz"))) for r in range(P)]
     parts = []
     for r in range(P):
         z = np.load(os.path.join(outdir, f"rank{r}.npz"))
@@ -76,3 +78,18 @@ def test_fitc_rccl_ranks_match_unsharded(gpu_ctx, tmp_path, P):
     from test_gpu_parity import fitc_cap
     _compare(parts, ref, _floor(X, y, Xt, yt, Z, th, True, gpu_ctx, ref), fitc_cap(Z, th),
              f"fitc_rccl_P{P}")
+
+
+@pytest.mark.parametrize("P,nfold,objective", [(2, 4, "kc"), (3, 6, "dss")])
+def test_fitc_blockloo_rccl_ranks(gpu_ctx, tmp_path, P, nfold, objective):
+    """FITC block-LOO with the rows sharded on fold boundaries over RCCL (the other ranks' Σ S_g in
+    one m×m all-reduce, the fold values and the gradient's n-sums): every rank returns the
+    unsharded value, fold values and θ- / Z-gradients within 30× the measured floor."""
+    args = (4000, 10, 40, 4, 45 + P)
+    raw = _rccl_ranks(P, tmp_path, args + ("block", nfold, objective), raw=True)
+    for r, z in enumerate(raw):
+        assert z["comm"].tolist() == [P, r] and str(z["kind"]) == "rccl"
+    parts = [(float(z["value"]), z["grad"], z["folds"], z["grad_Z"]) for z in raw]
+    X, y, _, _, Z, th = _case(*args)
+    _blockloo_check(gpu_ctx, X, y, Z, th, nfold, objective, parts,
+                    f"fitc_blockloo_rccl_P{P}_{objective}")

@@ -216,19 +216,14 @@ def _blockloo_sharded(P, X, y, Z, th, nfold, objective, rows):
         return list(ex.map(rank_job, range(P)))
 
 
-@pytest.mark.parametrize("P,nfold,objective", [(2, 4, "kc"), (3, 6, "dss"), (4, 4, "kc")])
-def test_fitc_blockloo_shards(gpu_ctx, P, nfold, objective):
-    """FITC block-LOO (K20:523-587 DSS, K20:655-720 KC) with the rows sharded on fold
-    boundaries (dist.fold_shard_rows): every rank returns the unsharded value, all fold values,
-    and the θ- and Z-gradients (a shard split only reorders the n-sums)."""
+def _blockloo_check(gpu_ctx, X, y, Z, th, nfold, objective, parts, tag):
+    """every rank's (value, folds, grad, grad_Z) against the unsharded block-LOO within 30× the
+    measured conditioning floor and under the absolute caps"""
     import gpscore
-    from gpscore.dist import fold_shard_rows
-    X, y, _, _, Z, th = _case(4000, 10, 40, 4, 45 + P)
     gp = gpscore.GP(ctx=gpu_ctx)
     gp.set_data(X, y, kind="fitc", Z=Z)
     v0, g0, f0, gz0 = gp.block_loo(th, objective, nfold=nfold, grad=True)
-    parts = _blockloo_sharded(P, X, y, Z, th, nfold, objective,
-                              lambda n, k, p, r: fold_shard_rows(n, k, p, r))
+
     def diffs(results):
         e = {}
         for res in results:
@@ -252,13 +247,26 @@ def test_fitc_blockloo_shards(gpu_ctx, P, nfold, objective):
     from test_gpu_parity import fitc_cap, fitc_grad_cap
     cap, gcap = fitc_cap(Z, th), fitc_grad_cap(Z, th, depth=4)  # block-LOO: 4 solves deep
     caps = {k: (gcap if k.startswith("grad") else cap) + 1e-13 for k in errs}
-    record_floors(f"fitc_blockloo_shards_P{P}_{objective}", errs, floor, caps)
+    record_floors(tag, errs, floor, caps)
     print(errs, floor, caps)
     bad = {k: (v, floor[k]) for k, v in errs.items() if v > 30.0 * floor[k] + 1e-13}
     assert not bad, bad
     # absolute ceilings on the values (fitc_cap) and the θ- / Z-gradients (fitc_grad_cap)
     over = {k: (errs[k], floor[k], caps[k]) for k in errs if max(errs[k], floor[k]) > caps[k]}
     assert not over, over
+
+
+@pytest.mark.parametrize("P,nfold,objective", [(2, 4, "kc"), (3, 6, "dss"), (4, 4, "kc")])
+def test_fitc_blockloo_shards(gpu_ctx, P, nfold, objective):
+    """FITC block-LOO (K20:523-587 DSS, K20:655-720 KC) with the rows sharded on fold
+    boundaries (dist.fold_shard_rows): every rank returns the unsharded value, all fold values,
+    and the θ- and Z-gradients (a shard split only reorders the n-sums)."""
+    from gpscore.dist import fold_shard_rows
+    X, y, _, _, Z, th = _case(4000, 10, 40, 4, 45 + P)
+    parts = _blockloo_sharded(P, X, y, Z, th, nfold, objective,
+                              lambda n, k, p, r: fold_shard_rows(n, k, p, r))
+    _blockloo_check(gpu_ctx, X, y, Z, th, nfold, objective, parts,
+                    f"fitc_blockloo_shards_P{P}_{objective}")
 
 
 def test_fitc_blockloo_refuses_straddling_folds(gpu_ctx):
