@@ -1579,7 +1579,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       return 0;
     case GPS_OPT_SLAB_XCD: g_slab_xcd = value != 0; return 0;
     case GPS_OPT_GEMM_PRIO: g_gemm_prio = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
-    case GPS_OPT_GRAM_REG: g_gram_reg = value != 0; return 0;
+    case GPS_OPT_GRAM_REG:
+      ARGCHK(value >= 0 && value <= 2, "GPS_OPT_GRAM_REG must be 0, 1 or 2");
+      g_gram_reg = value;
+      return 0;
     case GPS_OPT_GRAPH: ctx->graphs = value != 0; return 0;
     case GPS_OPT_PRED_PRE: ctx->pred_pre = value != 0; return 0;
     case GPS_OPT_DAG: ctx->dag = value != 0; return 0;

@@ -91,7 +91,8 @@ struct GemmParams {
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
 struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
-extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel
+extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel; 2: and
+                         //    rectangular d = 16 builds the matrix-core kernel
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 extern int g_stream_k;   // stream-K tail of uniform-K 128-tile launches (launch_gemm): 0 never,
                          // 1 every eligible launch, 2 (default) those marked sk_alone

@@ -17,6 +17,8 @@
 // matrix is diag(A, I) and its factor/inverse are diag(L, I) / diag(L⁻¹, I).
 #include "gps_internal.h"
 
+#include <type_traits>
+
 namespace gps {
 
 // 16-byte non-temporal store of an output pair (each element is written once and next read by
@@ -265,11 +267,198 @@ __global__ __launch_bounds__(256) void gram_col_kernel(GramParams p) {
     p.out[(int64_t)(r0 + rr) * p.ldo + gj] = 0.0;
 }
 
-int g_gram_reg = 1;  // GPS_OPT_GRAM_REG (process-wide; 0 = the LDS-column kernel for every d)
+// d = 16 builds on the matrix cores, in the reference's own form (ARD KF:15-22:
+// res = 2·x·x'ᵀ − ‖x‖² − ‖x'‖², then sf2·exp(½·res)): per 16×16 output block d/4
+// v_mfma_f64_16x16x4 for the cross products and ~20 VALU ops per element (two subtractions,
+// the exp, the scale) instead of the direct difference's 2d + 20 — at d = 16 the direct form is
+// VALU-bound (C5 Knm 3.9 TB/s).  Output differs from the direct-difference kernels by rounding
+// only: |Δres| ≲ ε·(‖x − c‖² + ‖x' − c‖²), with both sides shifted by the same point c — the
+// scaled features of the row tile's first row — so that an offset in the data (the reference's
+// uncentred expansion loses ε·‖x‖²) costs no more than in the direct difference.
+//
+// Persistent: the grid is sized to the chip and workgroup b takes the items (128×128 tiles,
+// row-major; with `lower` the tiles on or below the diagonal of a square build) [b·T/G,
+// (b+1)·T/G), so the row features' MFMA fragments and half norms are staged once per row tile
+// and the next column tile's features are in flight (registers) while the current one computes.
+// The scaled features of the tile's rows / columns sit in LDS with row stride d + 1 doubles (the
+// 16 rows a fragment read touches fall in distinct banks); thread t stages half a feature row
+// (row t/2, features (t&1)·d/2..) and the lane pair completes the row's squared norm.  Wave w
+// owns rows 32w..32w+31 of a tile and walks its 8 column blocks; each lane stores 4 rows × 1
+// column per block (the accumulator layout: 4 × 128 contiguous bytes per store instruction).
+// Diagonal tiles of a build with a diagonal add / identity padding / the lower mask, and tiles
+// with padded rows or columns, take the per-element selects; every other tile skips them.
+template <int D>
+__device__ __forceinline__ void gram_stage_half(const double* __restrict__ src, int rows_real,
+                                                int base, const double* inv_ell,
+                                                const double* __restrict__ cen, double (&v)[D / 2]) {
+  const int t = threadIdx.x, gi = base + (t >> 1), k0 = (t & 1) * (D / 2);
+#pragma unroll
+  for (int k = 0; k < D / 2; ++k)
+    v[k] = gi < rows_real ? src[(int64_t)gi * D + k0 + k] * inv_ell[k0 + k] -
+                                cen[k0 + k] * inv_ell[k0 + k]
+                          : 0.0;
+}
+template <int D>
+__device__ __forceinline__ void gram_put_half(double* xs, double* hs, const double (&v)[D / 2]) {
+  constexpr int LS = D + 1;
+  const int t = threadIdx.x, r = t >> 1, k0 = (t & 1) * (D / 2);
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < D / 2; ++k) {
+    xs[r * LS + k0 + k] = v[k];
+    s = fma(v[k], v[k], s);
+  }
+  s += __shfl_xor(s, 1);
+  if (!(t & 1)) hs[r] = 0.5 * s;  // ½‖x‖²: res/2 = x·x' − ½‖x‖² − ½‖x'‖², the same rounding
+}
+// item -> (row tile, column tile); lower: the lower-triangular tiles of a square build, row-major
+__device__ __forceinline__ void gram_item(int64_t it, int tiles_x, bool lower, int& by, int& bx) {
+  if (lower) {
+    int r = (int)((sqrt(8.0 * (double)it + 1.0) - 1.0) * 0.5);
+    while ((int64_t)r * (r + 1) / 2 > it) --r;
+    while ((int64_t)(r + 1) * (r + 2) / 2 <= it) ++r;
+    by = r;
+    bx = (int)(it - (int64_t)r * (r + 1) / 2);
+  } else {
+    by = (int)(it / tiles_x);
+    bx = (int)(it - (int64_t)by * tiles_x);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gram_mfma_kernel(GramParams p) {
+  static_assert(D % 8 == 0, "k-steps of 4, half rows");
+  constexpr int LS = D + 1;
+  __shared__ double xr[G2_ROWS * LS];
+  __shared__ double xc[GR_COLS * LS];
+  __shared__ double hr[G2_ROWS], hc[GR_COLS];
+  __shared__ double2 etab[64];
+  const int tiles_x = p.N / GR_COLS, tiles_m = (p.M + G2_ROWS - 1) / G2_ROWS;
+  const int64_t T = p.lower ? (int64_t)tiles_m * (tiles_m + 1) / 2 : (int64_t)tiles_m * tiles_x;
+  const int64_t it0 = (int64_t)blockIdx.x * T / gridDim.x, it1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const bool special = gram_diag_special(p);
+  exp_tab_stage(etab);
+  typedef double d4v __attribute__((ext_vector_type(4)));
+  double a[2][D / 4], pv[D / 2];
+  int cur_by = -1, by, bx;
+  if (it0 < it1) {
+    gram_item(it0, tiles_x, p.lower, by, bx);
+    gram_stage_half<D>(p.xp, p.m, bx * GR_COLS, p.inv_ell,
+                       p.x + (int64_t)min(by * G2_ROWS, p.n - 1) * D, pv);
+  }
+  for (int64_t it = it0; it < it1; ++it) {
+    gram_item(it, tiles_x, p.lower, by, bx);
+    const int c0 = bx * GR_COLS, r0 = by * G2_ROWS;
+    const int rows = min(G2_ROWS, p.M - r0);  // a multiple of 32 (launch_gram checks M % 32)
+    __syncthreads();  // the previous tile's reads of xc / hc / xr are done
+    if (by != cur_by) {
+      double rv[D / 2];
+      gram_stage_half<D>(p.x, p.n, r0, p.inv_ell, p.x + (int64_t)min(r0, p.n - 1) * D, rv);
+      gram_put_half<D>(xr, hr, rv);
+    }
+    gram_put_half<D>(xc, hc, pv);
+    __syncthreads();
+    if (by != cur_by) {
+      cur_by = by;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int rt = 32 * wave + 16 * rb;
+#pragma unroll
+        for (int kk = 0; kk < D / 4; ++kk) a[rb][kk] = xr[(rt + lr) * LS + 4 * kk + lg];
+      }
+    }
+    if (it + 1 < it1) {  // the next column tile's features, in flight while this one computes
+      int nby, nbx;
+      gram_item(it + 1, tiles_x, p.lower, nby, nbx);
+      gram_stage_half<D>(p.xp, p.m, nbx * GR_COLS, p.inv_ell,
+                         p.x + (int64_t)min(nby * G2_ROWS, p.n - 1) * D, pv);
+    }
+    if (32 * wave >= rows) continue;
+    const bool plain = r0 + rows <= p.n && c0 + GR_COLS <= p.m && !(bx == by && special);
+    const int rw = r0 + 32 * wave;
+    double* const obase = p.out + (int64_t)rw * p.ldo + c0;
+    // one column block of 16, row block rb: the cross products, then the elements
+    // (PLAIN: no selects; the edge tiles walk their row blocks one at a time, which keeps their
+    // selects within the plain path's registers)
+    auto rowblock = [&](int cb, int rb, const double (&b)[D / 4], double hcol, auto plain_tag) {
+      constexpr bool PLAIN = decltype(plain_tag)::value;
+      const int gj = c0 + 16 * cb + lr;
+      d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < D / 4; ++kk)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[rb][kk], b[kk], acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = 16 * rb + 4 * q + lg;
+        double v = p.sf2 * exp_neg((acc[q] - hr[32 * wave + rl]) - hcol, etab);
+        double* dst = obase + (int64_t)rl * p.ldo + 16 * cb + lr;
+        if constexpr (PLAIN) {
+          __builtin_nontemporal_store(v, dst);
+        } else {
+          const int gi = rw + rl;
+          if (gi == gj) v += p.diag_add;
+          if (gi >= p.n || gj >= p.m) v = (p.pad_identity && gi == gj) ? 1.0 : 0.0;
+          if (!p.lower || gj <= gi) __builtin_nontemporal_store(v, dst);
+        }
+      }
+    };
+    auto block = [&](int cb, auto plain_tag) {
+      constexpr bool PLAIN = decltype(plain_tag)::value;
+      double b[D / 4];
+#pragma unroll
+      for (int kk = 0; kk < D / 4; ++kk) b[kk] = xc[(16 * cb + lr) * LS + 4 * kk + lg];
+      const double hcol = hc[16 * cb + lr];
+      if constexpr (PLAIN) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) rowblock(cb, rb, b, hcol, plain_tag);
+      } else {
+#pragma unroll 1
+        for (int rb = 0; rb < 2; ++rb) rowblock(cb, rb, b, hcol, plain_tag);
+      }
+    };
+    if (plain) {
+#pragma unroll 1
+      for (int cb = 0; cb < GR_COLS / 16; ++cb) block(cb, std::true_type{});
+    } else {
+#pragma unroll 1
+      for (int cb = 0; cb < GR_COLS / 16; ++cb) block(cb, std::false_type{});
+    }
+  }
+}
+
+// GPS_OPT_GRAM_REG (process-wide): 0 = the LDS-column kernel for every d; 1 = the register-
+// resident direct-difference kernels for d in {1, 8, 16} (bitwise equal to 0); 2 (default) = as
+// 1 with the d = 16 builds on the matrix-core kernel.  (At d = 8 the matrix-core kernel is
+// slower than the direct difference — C3 K_ff 0.413 vs 0.369 ms, K*f 0.221 vs 0.206,
+// profiles/r5ah_gram_ab.json — the per-element VALU saving is 16 ops there, not 32.)
+int g_gram_reg = 2;
 
 hipError_t launch_gram(const GramParams& p, hipStream_t s) {
   if (p.d < 1 || p.d > GPS_MAX_D || p.M % GR_ROWS || p.N % GR_COLS || (p.ldo & 1))
     return hipErrorInvalidValue;
+  if (g_gram_reg == 2 && p.d == 16 && (!p.lower || p.M == p.N)) {
+    const int64_t tm = (p.M + G2_ROWS - 1) / G2_ROWS, tx = p.N / GR_COLS;
+    const int64_t items = p.lower ? tm * (tm + 1) / 2 : tm * tx;
+    if (items == 0) return hipSuccess;
+    // persistent over one resident wave of the grid (as many workgroups as fit on every CU at
+    // once); a build of fewer than 4 such waves of tiles runs one tile per workgroup instead
+    // (2-3 tiles per workgroup would leave the last round a third full: C5 K*m)
+    static int slots = 0;
+    if (!slots) {
+      int dev = 0, cus = 0, per = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)gram_mfma_kernel<16>, 256,
+                                                       0) != hipSuccess ||
+          cus < 1 || per < 1)
+        return hipErrorInvalidValue;
+      slots = cus * per;
+    }
+    const int64_t g = items < 4 * (int64_t)slots ? items : slots;
+    hipLaunchKernelGGL(gram_mfma_kernel<16>, dim3((unsigned)g), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   if (g_gram_reg && (p.d == 1 || p.d == 8 || p.d == 16)) {
     const int64_t blocks = (int64_t)((p.M + G2_ROWS - 1) / G2_ROWS) * (p.N / GR_COLS);
     if (blocks == 0) return hipSuccess;

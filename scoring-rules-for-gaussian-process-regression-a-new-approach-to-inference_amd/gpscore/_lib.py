@@ -226,9 +226,11 @@ class Context:
         self.call("gps_ctx_set_option", GPS_OPT_TINY_GEMM, 1 if on else 0)
 
     def set_gram_reg(self, on=True):
-        """Register-resident Gram kernel for d in {1, 8, 16} (default) or the LDS-column
-        kernel; bitwise-identical output (process-wide)."""
-        self.call("gps_ctx_set_option", GPS_OPT_GRAM_REG, 1 if on else 0)
+        """Gram kernels (process-wide): True / 2 (default) the register-resident kernels for
+        d in {1, 8, 16} with the rectangular d = 16 builds on the matrix cores; 1 the
+        register-resident kernels only (bitwise equal to 0); False / 0 the LDS-column kernel."""
+        v = on if isinstance(on, int) and not isinstance(on, bool) else (2 if on else 0)
+        self.call("gps_ctx_set_option", GPS_OPT_GRAM_REG, v)
 
     def set_graphs(self, on=True):
         """Replay the recursive factorisation from a captured hipGraph (default) or launch

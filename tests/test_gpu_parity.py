@@ -442,19 +442,21 @@ def test_not_positive_definite_raises(gp):
 @pytest.mark.parametrize("d", [1, 8, 16])
 @pytest.mark.parametrize("n,m,uplo", [(333, 201, 0), (333, 333, 1), (700, 520, 0), (640, 640, 1),
                                       (1000, 384, 0), (521, 521, 1)])
-def test_gram_reg_kernel_bitwise(gpu_ctx, d, n, m, uplo):
-    """The register-resident Gram kernels (d in {1, 8, 16}; at d = 16 the one-column interior
-    kernel plus the compact edge launch) against the LDS-column kernel: same arithmetic in the same
-    order, so bitwise-identical output, including the padded rows/columns (n, m not multiples of
-    128, and exact multiples), the lower mask and the diagonal add."""
+def test_gram_kernels(gpu_ctx, d, n, m, uplo):
+    """GPS_OPT_GRAM_REG 1, the register-resident direct-difference kernels (d in {1, 8, 16}; at
+    d = 16 the one-column interior kernel plus the compact edge launch), against 0, the
+    LDS-column kernel: same arithmetic in the same order, so bitwise-identical output.  Mode 2
+    (the default: d = 16 on the matrix cores in the reference's expansion, KF:15-22) against
+    the oracle within the expansion's rounding, and bitwise equal to mode 1 at d = 1, 8.  All three with padded rows/columns (n,
+    m not multiples of 128, and exact multiples), the lower mask and the diagonal add."""
     from gpscore._lib import GPS_ARD, ptr
     rng = np.random.default_rng(10 + d)
     x = rng.standard_normal((n, d))
     xp = x if uplo else rng.standard_normal((m, d))
     ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
     outs = []
-    for on in (False, True):
-        gpu_ctx.set_gram_reg(on)
+    for mode in (0, 1, 2):
+        gpu_ctx.set_gram_reg(mode)
         out = np.full((n, m), -7.0)
         gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), n, ptr(xp), m, d, 0.3, ptr(ell), d, 0.01,
                      uplo, ptr(out))
@@ -463,9 +465,99 @@ def test_gram_reg_kernel_bitwise(gpu_ctx, d, n, m, uplo):
     assert np.array_equal(outs[0], outs[1])
     ref = O.fast_gram(x, xp, 0.3, ell) + 0.01 * np.eye(n, m)  # diag_add goes on i == j
     mask = np.tril(np.ones((n, m), bool)) if uplo else np.ones((n, m), bool)
-    assert nrel(outs[1][mask], ref[mask]) < 1e-13
-    if uplo:
-        assert np.all(outs[1][~mask] == 0.0)  # gps_gram zero-fills the unwritten half
+    for out in outs[1:]:
+        assert nrel(out[mask], ref[mask]) < 1e-13
+        if uplo:
+            assert np.all(out[~mask] == 0.0)  # gps_gram zero-fills the unwritten half
+    if d != 16:
+        assert np.array_equal(outs[2], outs[1])  # d = 1, 8 stay on the register kernels
+
+
+@pytest.mark.parametrize("n,m", [(333, 201), (700, 520), (1000, 384), (128, 4096), (2049, 129),
+                                 (20000, 4096)])
+def test_gram_mfma_kernel(gpu_ctx, n, m):
+    """The matrix-core kernel (GPS_OPT_GRAM_REG 2, the default at d = 16) in the
+    reference's own expansion (ARD KF:15-22: 2·x·x'ᵀ − ‖x‖² − ‖x'‖², halved, exp, × sf2):
+    against that expansion restated in numpy and the direct-difference oracle, within its
+    rounding (|Δres| ≲ ε·(‖x‖² + ‖x'‖²): 1e-13 normwise), and against the direct-difference
+    kernels (mode 1) likewise — and not bitwise equal to them (the matrix-core path ran).
+    20000 × 4096: 5000 tiles, the persistent grid (each workgroup a run of tiles)."""
+    from gpscore._lib import GPS_ARD, ptr
+    d = 16
+    rng = np.random.default_rng(n + m + d)
+    x, xp = rng.standard_normal((n, d)), rng.standard_normal((m, d))
+    ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
+    outs = {}
+    for mode in (1, 2):
+        gpu_ctx.set_gram_reg(mode)
+        out = np.full((n, m), -7.0)
+        gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), n, ptr(xp), m, d, 0.3, ptr(ell), d, 0.0, 0,
+                     ptr(out))
+        outs[mode] = out
+    gpu_ctx.set_gram_reg(True)
+    xs, xps = x / np.exp(ell), xp / np.exp(ell)
+    res = 2 * xs @ xps.T - (xs * xs).sum(1)[:, None] - (xps * xps).sum(1)[None, :]
+    expansion = np.exp(0.3) * np.exp(0.5 * res)
+    assert nrel(outs[2], expansion) < 1e-13
+    assert nrel(outs[2], O.fast_gram(x, xp, 0.3, ell)) < 1e-13
+    assert nrel(outs[2], outs[1]) < 1e-13
+    assert np.all(np.isfinite(outs[2])) and not np.array_equal(outs[2], outs[1])
+
+
+@pytest.mark.parametrize("n,m,uplo", [(700, 520, 0), (640, 640, 1), (9000, 4096, 0)])
+def test_gram_mfma_offset_data(gpu_ctx, n, m, uplo):
+    """Data far from the origin (features around 200): the reference's uncentred expansion would
+    lose ε·‖x/ℓ‖² ≈ 1e-10 in the exponent; the matrix-core kernel shifts both sides by the row
+    tile's first point, so it stays within the direct difference's own error of the oracle."""
+    from gpscore._lib import GPS_ARD, ptr
+    d = 16
+    rng = np.random.default_rng(n + 5 * m)
+    x = 200.0 + rng.standard_normal((n, d))
+    xp = x if uplo else 200.0 + rng.standard_normal((m, d))
+    ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
+    outs = {}
+    for mode in (1, 2):
+        gpu_ctx.set_gram_reg(mode)
+        out = np.full((n, m), -7.0)
+        gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), n, ptr(xp), m, d, 0.3, ptr(ell), d, 0.0, uplo,
+                     ptr(out))
+        outs[mode] = out
+    gpu_ctx.set_gram_reg(True)
+    rows = np.arange(0, n, max(1, n // 500))
+    ref = O.fast_gram(x[rows], xp, 0.3, ell)
+    mask = (np.arange(m)[None, :] <= rows[:, None]) if uplo else np.ones(ref.shape, bool)
+    e1 = nrel(outs[1][rows][mask], ref[mask])
+    e2 = nrel(outs[2][rows][mask], ref[mask])
+    assert e2 < 1e-13 and e2 < 10 * e1 + 1e-15, (e1, e2)
+
+
+def test_gram_mfma_lower_persistent(gpu_ctx):
+    """A lower d = 16 build large enough for the persistent grid (n = 11 648: 91 tile rows,
+    4186 lower tiles, several per workgroup, row changes inside a workgroup's run) with the
+    diagonal add: against the direct-difference kernels on the lower triangle, the upper half
+    unwritten, and sampled rows against the oracle."""
+    from gpscore._lib import GPS_ARD, ptr
+    n, d = 11648, 16
+    rng = np.random.default_rng(77)
+    x = rng.standard_normal((n, d))
+    ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
+    outs = {}
+    for mode in (1, 2):
+        gpu_ctx.set_gram_reg(mode)
+        out = np.full((n, n), -7.0)
+        gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), n, ptr(x), n, d, 0.3, ptr(ell), d, 0.01, 1,
+                     ptr(out))
+        outs[mode] = out
+    gpu_ctx.set_gram_reg(True)
+    iu = np.triu_indices(n, 1)
+    assert np.all(outs[2][iu] == 0.0)
+    a, b = np.tril(outs[2]), np.tril(outs[1])
+    assert nrel(a, b) < 1e-13 and not np.array_equal(a, b)
+    rows = rng.choice(n, 64, replace=False)
+    ref = O.fast_gram(x[rows], x, 0.3, ell)
+    ref[np.arange(64), rows] += 0.01
+    for r, i in enumerate(rows):
+        assert nrel(outs[2][i, :i + 1], ref[r, :i + 1]) < 1e-13
 
 
 def test_gram_kernel(gpu_ctx):

@@ -1,5 +1,6 @@
 """Gram kernel timings (gram_kff / gram_ksf at C3, gram_knm at C5) of the library this process
-loads (GPSCORE_LIB selects a variant build): hipEvent records over 5 fits, single stream."""
+loads (GPSCORE_LIB selects a variant build): hipEvent records over 5 fits, single stream, for
+each GPS_OPT_GRAM_REG mode given on the command line (default: 1 2)."""
 import json
 import os
 import sys
@@ -12,7 +13,9 @@ import gpscore  # noqa: E402
 
 ctx = gpscore.Context(0)
 out = {"lib": os.environ.get("GPSCORE_LIB", "in-tree")}
-for cfg in ("C3", "C5"):
+modes = [int(a) for a in sys.argv[1:]] or [1, 2]
+for cfg, mode in [(c, md) for c in ("C3", "C5") for md in modes]:
+    ctx.set_gram_reg(mode)
     c = bench.CONFIGS[cfg]
     X, y, Xt, yt, Z, th = bench.synth(c["n"], c["d"], c["nt"], c["seed"], c.get("m"))
     gp = gpscore.GP(ctx=ctx)
@@ -32,5 +35,5 @@ for cfg in ("C3", "C5"):
     ctx.set_overlap(True)
     for k, v in rep.items():
         if k.startswith("gram"):
-            out[f"{cfg}.{k}"] = {"ms": v["ms"] / v["count"], "GB/s": v["bytes"] / (v["ms"] * 1e-3) / 1e9}
+            out[f"{cfg}.{k}.mode{mode}"] = {"ms": v["ms"] / v["count"], "GB/s": v["bytes"] / (v["ms"] * 1e-3) / 1e9}
 print(json.dumps(out))
