@@ -303,7 +303,7 @@ def roofline_gram(prof, steps=1, traffic=None, tags=("gram_kff", "gram_ksf")):
     b = sum(prof[t]["bytes"] for t in tags if t in prof) / steps
     ms = sum(prof[t]["ms"] for t in tags if t in prof) / steps
     ach = b / (ms * 1e-3) / 1e9 if ms else 0.0
-    return {"bound": "hbm", "kernel": "gram_reg_kernel<8> (K_ff lower + K*f)", "achieved": round(ach, 1),
+    return {"bound": "hbm", "kernel": "gram_mfma_kernel<8> (K_ff lower + K*f)", "achieved": round(ach, 1),
             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
             "traffic": traffic, "traffic_kind": TRAFFIC_KIND if traffic is not None else None,
             "bytes_per_step": b,

@@ -85,9 +85,9 @@ enum {
                             use the small kernel (16/32-blocks per wave, K split over the waves
                             of a workgroup, no LDS staging, no reduce launch); 0: the 64-tile
                             split-K + reduce path for them.  Process-wide. */
-  GPS_OPT_GRAM_REG = 9,  /* 2 (default): as 1, with the d = 16 builds on the matrix cores in
-                            the reference's expansion 2·x·x'ᵀ − ‖x‖² − ‖x'‖² (KF:15-22; equal
-                            to 1 within its rounding); 1: Gram builds with d in {1, 8, 16}
+  GPS_OPT_GRAM_REG = 9,  /* 2 (default): as 1, with the d = 8, 16 builds on the matrix cores
+                            in the reference's expansion 2·x·x'ᵀ − ‖x‖² − ‖x'‖² (KF:15-22;
+                            equal to 1 within its rounding); 1: Gram builds with d in {1, 8, 16}
                             keep the column features in registers (128×128 tiles); 0: the
                             LDS-column kernel (bitwise equal to 1).  Process-wide. */
   GPS_OPT_GRAPH = 10,    /* 1 (default): the recursive factorisation's launch sequence is

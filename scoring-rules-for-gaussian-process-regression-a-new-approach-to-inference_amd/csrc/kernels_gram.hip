@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void gram_col_kernel(GramParams p) {
     p.out[(int64_t)(r0 + rr) * p.ldo + gj] = 0.0;
 }
 
-// d = 16 builds on the matrix cores, in the reference's own form (ARD KF:15-22:
+// d = 8 / 16 builds on the matrix cores, in the reference's own form (ARD KF:15-22:
 // res = 2·x·x'ᵀ − ‖x‖² − ‖x'‖², then sf2·exp(½·res)): per 16×16 output block d/4
 // v_mfma_f64_16x16x4 for the cross products and ~20 VALU ops per element (two subtractions,
 // the exp, the scale) instead of the direct difference's 2d + 20 — at d = 16 the direct form is
@@ -277,9 +277,11 @@ __global__ __launch_bounds__(256) void gram_col_kernel(GramParams p) {
 // uncentred expansion loses ε·‖x‖²) costs no more than in the direct difference.
 //
 // Persistent: the grid is sized to the chip and workgroup b takes the items (128×128 tiles,
-// row-major; with `lower` the tiles on or below the diagonal of a square build) [b·T/G,
-// (b+1)·T/G), so the row features' MFMA fragments and half norms are staged once per row tile
-// and the next column tile's features are in flight (registers) while the current one computes.
+// row-major; with `lower` the tiles on or below the diagonal of a square build) either as the
+// contiguous run [b·T/G, (b+1)·T/G) (S = false: the row features' MFMA fragments and half norms
+// are staged once per row tile) or strided b, b + G, ... (S: the workgroups resident at one time
+// write neighbouring tiles, each item restages its rows); either way the next item's features
+// are in flight (registers) while the current one computes.
 // The scaled features of the tile's rows / columns sit in LDS with row stride d + 1 doubles (the
 // 16 rows a fragment read touches fall in distinct banks); thread t stages half a feature row
 // (row t/2, features (t&1)·d/2..) and the lane pair completes the row's squared norm.  Wave w
@@ -325,7 +327,7 @@ __device__ __forceinline__ void gram_item(int64_t it, int tiles_x, bool lower, i
   }
 }
 
-template <int D>
+template <int D, bool S>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gram_mfma_kernel(GramParams p) {
   static_assert(D % 8 == 0, "k-steps of 4, half rows");
   constexpr int LS = D + 1;
@@ -335,27 +337,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   __shared__ double2 etab[64];
   const int tiles_x = p.N / GR_COLS, tiles_m = (p.M + G2_ROWS - 1) / G2_ROWS;
   const int64_t T = p.lower ? (int64_t)tiles_m * (tiles_m + 1) / 2 : (int64_t)tiles_m * tiles_x;
-  const int64_t it0 = (int64_t)blockIdx.x * T / gridDim.x, it1 = (int64_t)(blockIdx.x + 1) * T / gridDim.x;
+  // S: items blockIdx.x, + gridDim.x, ... (the workgroups resident at one time write neighbouring
+  // tiles); otherwise the contiguous run [b·T/G, (b+1)·T/G)
+  const int64_t step = S ? gridDim.x : 1;
+  const int64_t end = S ? T : (int64_t)(blockIdx.x + 1) * T / gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const bool special = gram_diag_special(p);
   exp_tab_stage(etab);
   typedef double d4v __attribute__((ext_vector_type(4)));
-  double a[2][D / 4], pv[D / 2];
+  double a[2][D / 4], pv[D / 2], qv[S ? D / 2 : 1];
   int cur_by = -1, by, bx;
-  if (it0 < it1) {
-    gram_item(it0, tiles_x, p.lower, by, bx);
-    gram_stage_half<D>(p.xp, p.m, bx * GR_COLS, p.inv_ell,
-                       p.x + (int64_t)min(by * G2_ROWS, p.n - 1) * D, pv);
+  int64_t it = S ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * T / gridDim.x;
+  auto stage_next = [&](int nby, int nbx) {  // the item's column (and with S its row) features
+    const double* cen = p.x + (int64_t)min(nby * G2_ROWS, p.n - 1) * D;
+    gram_stage_half<D>(p.xp, p.m, nbx * GR_COLS, p.inv_ell, cen, pv);
+    if constexpr (S) gram_stage_half<D>(p.x, p.n, nby * G2_ROWS, p.inv_ell, cen, qv);
+  };
+  if (it < end) {
+    gram_item(it, tiles_x, p.lower, by, bx);
+    stage_next(by, bx);
   }
-  for (int64_t it = it0; it < it1; ++it) {
+  for (; it < end; it += step) {
     gram_item(it, tiles_x, p.lower, by, bx);
     const int c0 = bx * GR_COLS, r0 = by * G2_ROWS;
     const int rows = min(G2_ROWS, p.M - r0);  // a multiple of 32 (launch_gram checks M % 32)
     __syncthreads();  // the previous tile's reads of xc / hc / xr are done
     if (by != cur_by) {
-      double rv[D / 2];
-      gram_stage_half<D>(p.x, p.n, r0, p.inv_ell, p.x + (int64_t)min(r0, p.n - 1) * D, rv);
-      gram_put_half<D>(xr, hr, rv);
+      if constexpr (S) {
+        gram_put_half<D>(xr, hr, qv);
+      } else {
+        double rv[D / 2];
+        gram_stage_half<D>(p.x, p.n, r0, p.inv_ell, p.x + (int64_t)min(r0, p.n - 1) * D, rv);
+        gram_put_half<D>(xr, hr, rv);
+      }
     }
     gram_put_half<D>(xc, hc, pv);
     __syncthreads();
@@ -368,11 +382,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
         for (int kk = 0; kk < D / 4; ++kk) a[rb][kk] = xr[(rt + lr) * LS + 4 * kk + lg];
       }
     }
-    if (it + 1 < it1) {  // the next column tile's features, in flight while this one computes
+    if (it + step < end) {  // the next item's features, in flight while this one computes
       int nby, nbx;
-      gram_item(it + 1, tiles_x, p.lower, nby, nbx);
-      gram_stage_half<D>(p.xp, p.m, nbx * GR_COLS, p.inv_ell,
-                         p.x + (int64_t)min(nby * G2_ROWS, p.n - 1) * D, pv);
+      gram_item(it + step, tiles_x, p.lower, nby, nbx);
+      stage_next(nby, nbx);
     }
     if (32 * wave >= rows) continue;
     const bool plain = r0 + rows <= p.n && c0 + GR_COLS <= p.m && !(bx == by && special);
@@ -429,35 +442,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 
 // GPS_OPT_GRAM_REG (process-wide): 0 = the LDS-column kernel for every d; 1 = the register-
 // resident direct-difference kernels for d in {1, 8, 16} (bitwise equal to 0); 2 (default) = as
-// 1 with the d = 16 builds on the matrix-core kernel.  (At d = 8 the matrix-core kernel is
-// slower than the direct difference — C3 K_ff 0.413 vs 0.369 ms, K*f 0.221 vs 0.206,
-// profiles/r5ah_gram_ab.json — the per-element VALU saving is 16 ops there, not 32.)
+// 1 with the d = 8 and 16 builds on the matrix-core kernel (C3 K_ff 0.383 -> 0.351 ms, K*f
+// 0.220 -> 0.192, C5 Knm 1.70 -> 1.47: profiles/r5am_gram_ab.json)
 int g_gram_reg = 2;
 
 hipError_t launch_gram(const GramParams& p, hipStream_t s) {
   if (p.d < 1 || p.d > GPS_MAX_D || p.M % GR_ROWS || p.N % GR_COLS || (p.ldo & 1))
     return hipErrorInvalidValue;
-  if (g_gram_reg == 2 && p.d == 16 && (!p.lower || p.M == p.N)) {
+  if (g_gram_reg == 2 && (p.d == 8 || p.d == 16) && (!p.lower || p.M == p.N)) {
     const int64_t tm = (p.M + G2_ROWS - 1) / G2_ROWS, tx = p.N / GR_COLS;
     const int64_t items = p.lower ? tm * (tm + 1) / 2 : tm * tx;
     if (items == 0) return hipSuccess;
+    // d = 16 walks contiguous runs of tiles (row fragments staged once per row tile), d = 8
+    // strided items (the resident workgroups write neighbouring tiles; its staging is half as
+    // large): C5 Knm 1.47 vs 1.87 ms, C3 K_ff 0.351 vs 0.390 and K*f 0.192 vs 0.225 ms the
+    // other way round (profiles/r5am_gram_ab.json, mode 2 = contiguous at both, 3 = strided)
+    const void* fn = p.d == 8 ? (const void*)gram_mfma_kernel<8, true> : (const void*)gram_mfma_kernel<16, false>;
     // persistent over one resident wave of the grid (as many workgroups as fit on every CU at
     // once); a build of fewer than 4 such waves of tiles runs one tile per workgroup instead
     // (2-3 tiles per workgroup would leave the last round a third full: C5 K*m)
-    static int slots = 0;
-    if (!slots) {
+    static int slots[2] = {0, 0};
+    int& sl = slots[p.d == 16];
+    if (!sl) {
       int dev = 0, cus = 0, per = 0;
       if (hipGetDevice(&dev) != hipSuccess ||
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)gram_mfma_kernel<16>, 256,
-                                                       0) != hipSuccess ||
-          cus < 1 || per < 1)
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || cus < 1 ||
+          per < 1)
         return hipErrorInvalidValue;
-      slots = cus * per;
+      sl = cus * per;
     }
-    const int64_t g = items < 4 * (int64_t)slots ? items : slots;
-    hipLaunchKernelGGL(gram_mfma_kernel<16>, dim3((unsigned)g), dim3(256), 0, s, p);
-    return hipGetLastError();
+    const int64_t g = items < 4 * (int64_t)sl ? items : sl;
+    GramParams q = p;
+    void* args[] = {&q};
+    return hipLaunchKernel(fn, dim3((unsigned)g), dim3(256), args, 0, s);
   }
   if (g_gram_reg && (p.d == 1 || p.d == 8 || p.d == 16)) {
     const int64_t blocks = (int64_t)((p.M + G2_ROWS - 1) / G2_ROWS) * (p.N / GR_COLS);

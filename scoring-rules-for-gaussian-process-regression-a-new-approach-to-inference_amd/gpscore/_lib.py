@@ -226,9 +226,10 @@ class Context:
         self.call("gps_ctx_set_option", GPS_OPT_TINY_GEMM, 1 if on else 0)
 
     def set_gram_reg(self, on=True):
-        """Gram kernels (process-wide): True / 2 (default) the register-resident kernels for
-        d in {1, 8, 16} with the rectangular d = 16 builds on the matrix cores; 1 the
-        register-resident kernels only (bitwise equal to 0); False / 0 the LDS-column kernel."""
+        """Gram kernels (process-wide): True / 2 (default) the d = 8, 16 builds on the matrix
+        cores (the reference's expansion, centred), d = 1 on the register-resident kernel; 1 the
+        register-resident direct-difference kernels (bitwise equal to 0); False / 0 the
+        LDS-column kernel."""
         v = on if isinstance(on, int) and not isinstance(on, bool) else (2 if on else 0)
         self.call("gps_ctx_set_option", GPS_OPT_GRAM_REG, v)
 

@@ -446,8 +446,8 @@ def test_gram_kernels(gpu_ctx, d, n, m, uplo):
     """GPS_OPT_GRAM_REG 1, the register-resident direct-difference kernels (d in {1, 8, 16}; at
     d = 16 the one-column interior kernel plus the compact edge launch), against 0, the
     LDS-column kernel: same arithmetic in the same order, so bitwise-identical output.  Mode 2
-    (the default: d = 16 on the matrix cores in the reference's expansion, KF:15-22) against
-    the oracle within the expansion's rounding, and bitwise equal to mode 1 at d = 1, 8.  All three with padded rows/columns (n,
+    (the default: d = 8, 16 on the matrix cores in the reference's expansion, KF:15-22) against
+    the oracle within the expansion's rounding, and bitwise equal to mode 1 at d = 1.  All three with padded rows/columns (n,
     m not multiples of 128, and exact multiples), the lower mask and the diagonal add."""
     from gpscore._lib import GPS_ARD, ptr
     rng = np.random.default_rng(10 + d)
@@ -469,21 +469,22 @@ def test_gram_kernels(gpu_ctx, d, n, m, uplo):
         assert nrel(out[mask], ref[mask]) < 1e-13
         if uplo:
             assert np.all(out[~mask] == 0.0)  # gps_gram zero-fills the unwritten half
-    if d != 16:
-        assert np.array_equal(outs[2], outs[1])  # d = 1, 8 stay on the register kernels
+    if d == 1:
+        assert np.array_equal(outs[2], outs[1])  # d = 1 stays on the register kernel
 
 
+@pytest.mark.parametrize("d", [8, 16])
 @pytest.mark.parametrize("n,m", [(333, 201), (700, 520), (1000, 384), (128, 4096), (2049, 129),
                                  (20000, 4096)])
-def test_gram_mfma_kernel(gpu_ctx, n, m):
-    """The matrix-core kernel (GPS_OPT_GRAM_REG 2, the default at d = 16) in the
+def test_gram_mfma_kernel(gpu_ctx, d, n, m):
+    """The matrix-core kernel (GPS_OPT_GRAM_REG 2, the default at d = 8, 16) in the
     reference's own expansion (ARD KF:15-22: 2·x·x'ᵀ − ‖x‖² − ‖x'‖², halved, exp, × sf2):
     against that expansion restated in numpy and the direct-difference oracle, within its
     rounding (|Δres| ≲ ε·(‖x‖² + ‖x'‖²): 1e-13 normwise), and against the direct-difference
     kernels (mode 1) likewise — and not bitwise equal to them (the matrix-core path ran).
-    20000 × 4096: 5000 tiles, the persistent grid (each workgroup a run of tiles)."""
+    20000 × 4096: 5000 tiles, the persistent grid (d = 16 each workgroup a contiguous run of
+    tiles, d = 8 strided items)."""
     from gpscore._lib import GPS_ARD, ptr
-    d = 16
     rng = np.random.default_rng(n + m + d)
     x, xp = rng.standard_normal((n, d)), rng.standard_normal((m, d))
     ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
@@ -504,14 +505,14 @@ def test_gram_mfma_kernel(gpu_ctx, n, m):
     assert np.all(np.isfinite(outs[2])) and not np.array_equal(outs[2], outs[1])
 
 
-@pytest.mark.parametrize("n,m,uplo", [(700, 520, 0), (640, 640, 1), (9000, 4096, 0)])
-def test_gram_mfma_offset_data(gpu_ctx, n, m, uplo):
+@pytest.mark.parametrize("d", [8, 16])
+@pytest.mark.parametrize("n,m,uplo", [(700, 520, 0), (640, 640, 1), (20000, 4096, 0)])
+def test_gram_mfma_offset_data(gpu_ctx, d, n, m, uplo):
     """Data far from the origin (features around 200): the reference's uncentred expansion would
     lose ε·‖x/ℓ‖² ≈ 1e-10 in the exponent; the matrix-core kernel shifts both sides by the row
     tile's first point, so it stays within the direct difference's own error of the oracle."""
     from gpscore._lib import GPS_ARD, ptr
-    d = 16
-    rng = np.random.default_rng(n + 5 * m)
+    rng = np.random.default_rng(n + 5 * m + d)
     x = 200.0 + rng.standard_normal((n, d))
     xp = x if uplo else 200.0 + rng.standard_normal((m, d))
     ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)
@@ -531,13 +532,14 @@ def test_gram_mfma_offset_data(gpu_ctx, n, m, uplo):
     assert e2 < 1e-13 and e2 < 10 * e1 + 1e-15, (e1, e2)
 
 
-def test_gram_mfma_lower_persistent(gpu_ctx):
-    """A lower d = 16 build large enough for the persistent grid (n = 11 648: 91 tile rows,
-    4186 lower tiles, several per workgroup, row changes inside a workgroup's run) with the
-    diagonal add: against the direct-difference kernels on the lower triangle, the upper half
-    unwritten, and sampled rows against the oracle."""
+@pytest.mark.parametrize("d", [8, 16])
+def test_gram_mfma_lower_persistent(gpu_ctx, d):
+    """A lower build large enough for the persistent grid (n = 11 648: 91 tile rows, 4186 lower
+    tiles, several per workgroup, row changes inside a workgroup's run) with the diagonal add:
+    against the direct-difference kernels on the lower triangle, the upper half unwritten, and
+    sampled rows against the oracle."""
     from gpscore._lib import GPS_ARD, ptr
-    n, d = 11648, 16
+    n = 11648
     rng = np.random.default_rng(77)
     x = rng.standard_normal((n, d))
     ell = np.ascontiguousarray(rng.standard_normal(d) * 0.2)

@@ -2,7 +2,7 @@
 the main stream's busy time by kernel class, the idle gaps before each class (what the main
 stream waited on: launch boundaries, the side stream's join, the host), and the side stream.
 Usage: python tools/critpath.py <run_kernel_trace.csv> [unit_index]
-Units are delimited by the K_ff Gram launches (gram_reg_kernel<8>, the largest grid)."""
+Units are delimited by the K_ff Gram launches (gram_mfma_kernel<8, true>, gram_reg_kernel<8> before round 5)."""
 import csv
 import sys
 from collections import defaultdict
@@ -22,7 +22,7 @@ for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                  int(r["Queue_Id"]), int(r["Queue_Id"]), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"])))
 rows.sort()
-kff = [i for i, k in enumerate(rows) if "gram_reg_kernel<8>" in k[2] and k[5] > 5_000_000]
+kff = [i for i, k in enumerate(rows) if ("gram_reg_kernel<8>" in k[2] or "gram_mfma_kernel<8" in k[2]) and k[5] > 5_000_000]
 u = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 a = kff[u]
 b = kff[u + 1] if u + 1 < len(kff) else len(rows)

@@ -27,7 +27,8 @@ for cfg, mode in [(c, md) for c in ("C3", "C5") for md in modes]:
     gp.fit(theta=th, return_loo=False)
     ctx.set_overlap(False)
     ctx.prof(True)
-    for _ in range(5):
+    reps = int(os.environ.get("GRAM_AB_REPS", "5"))
+    for _ in range(reps):
         gp.fit(theta=th, return_loo=False)
         gp.predict()
     rep = ctx.prof_collect()
@@ -35,5 +36,6 @@ for cfg, mode in [(c, md) for c in ("C3", "C5") for md in modes]:
     ctx.set_overlap(True)
     for k, v in rep.items():
         if k.startswith("gram"):
-            out[f"{cfg}.{k}.mode{mode}"] = {"ms": v["ms"] / v["count"], "GB/s": v["bytes"] / (v["ms"] * 1e-3) / 1e9}
+            out[f"{cfg}.{k}.mode{mode}"] = {"ms": v["ms"] / v["count"], "GB/s": v["bytes"] / (v["ms"] * 1e-3) / 1e9,
+                                            **({"max_ms": v["max_ms"]} if "max_ms" in v else {})}
 print(json.dumps(out))

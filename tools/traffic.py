@@ -65,7 +65,7 @@ def main(d, sub=""):
     # part of the roofline's launch set, bench.roofline_mfma)
     summary["_roofline"] = {"gemm_per_launch_bytes": avg("gps::gemm_f64_kernel", "gps::gemm_f64_small_kernel",
                                                          "gps::dag::potrf_dag_kernel"),
-                            "gram_per_launch_bytes": avg("gps::gram_kernel", "gps::gram_reg_kernel"),
+                            "gram_per_launch_bytes": avg("gps::gram_kernel", "gps::gram_reg_kernel", "gps::gram_mfma_kernel"),
                             "kind": "L2-fabric bytes (TCC FETCH_SIZE + WRITE_SIZE: every L2 miss, "
                                     "Infinity-Cache hits included) — an upper bound on HBM bytes",
                             "note": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "

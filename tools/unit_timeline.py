@@ -10,7 +10,7 @@ ks = []
 for r in csv.DictReader(open(sys.argv[1])):
     ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
 ks.sort()
-kff = [i for i, k in enumerate(ks) if ("gram_kernel<8>" in k[2] or "gram_reg_kernel<8>" in k[2]) and k[1] - k[0] > 300000]
+kff = [i for i, k in enumerate(ks) if ("gram_kernel<8>" in k[2] or "gram_reg_kernel<8>" in k[2] or "gram_mfma_kernel<8" in k[2]) and k[1] - k[0] > 300000]
 u = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 a, b = kff[u], kff[u + 1]
 win = ks[a:b]
