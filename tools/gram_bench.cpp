@@ -1,8 +1,11 @@
-// Gram-build microbenchmark (round 5): the library's gram_reg_kernel<8> (csrc/kernels_gram.hip) on
-// the C3 shapes — K_ff lower (20000², d = 8) and K*f (5000 × 20000) — against variants of its
-// interior-tile loop on the K*f shape: store-only (the access pattern's ceiling), 256 columns per
-// workgroup, 64 rows per workgroup, 4 rows per unrolled step.  Bitwise check of each variant's
-// output against the library's.
+// Gram-build microbenchmark (round 5): the library's d = 8 Gram (csrc/kernels_gram.hip: the
+// direct-difference gram_reg_kernel<8> until the matrix-core gram_mfma_kernel<8, true> replaced it)
+// on the C3 shapes — K_ff lower (20000², d = 8) and K*f (5000 × 20000) — against variants of the
+// register kernel's interior-tile loop on the K*f shape (store-only: the access pattern's ceiling,
+// 256 columns per workgroup, 64 rows per workgroup, 4 rows per unrolled step; bitwise check
+// against the library, which only holds while the library is that kernel) and store-only kernels
+// with the matrix-core kernel's output layout (profiles/r5ap_gram_bench.txt: 5.39 TB/s, the
+// 16-byte-row pattern 5.50).
 //   hipcc -O3 --offload-arch=gfx950 -I include -I <pkg>/csrc tools/gram_bench.cpp -o tbin/gram_bench
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -122,6 +125,39 @@ __global__ __launch_bounds__(256) void gram_one_col(GramParams p) {
     if (EXPAND) a = fmax(fma(-2.0, a, rn[rr] + fn), 0.0);
     __builtin_nontemporal_store(p.sf2 * exp_neg(-0.5 * a, etab), p.out + (int64_t)(r0 + rr) * p.ldo + gj);
   }
+}
+
+// store-only with the matrix-core kernel's output layout: per 16-column block each lane stores
+// 8 bytes to 4 rows (v_mfma_f64_16x16x4 accumulator order: 4 × 128 contiguous bytes per store
+// instruction); PAIR: lane pairs swap halves first (one __shfl_xor) so that each lane stores 16
+// bytes to 2 rows (2 × 256 bytes per instruction)
+template <bool PAIR>
+__global__ __launch_bounds__(256) void store_mfma_layout(GramParams p) {
+  const int tiles_x = p.N / 128;
+  const int c0 = (blockIdx.x % tiles_x) * 128, r0 = (blockIdx.x / tiles_x) * 128;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lg = lane >> 4;
+  double* const obase = p.out + (int64_t)(r0 + 32 * wave) * p.ldo + c0;
+  for (int cb = 0; cb < 8; ++cb)
+    for (int rb = 0; rb < 2; ++rb) {
+      double v[4];
+      for (int q = 0; q < 4; ++q) v[q] = p.sf2 + q + lr;
+      if constexpr (PAIR) {
+        // even lane keeps rows q = 0,1 and takes the odd lane's, odd lane rows 2,3
+        const bool odd = lr & 1;
+        const double s0 = __shfl_xor(odd ? v[0] : v[2], 1), s1 = __shfl_xor(odd ? v[1] : v[3], 1);
+        const int c = 16 * cb + (lr & ~1);
+        typedef double nv2 __attribute__((ext_vector_type(2)));
+        for (int h = 0; h < 2; ++h) {
+          const int q = odd ? 2 + h : h;
+          const double mine = v[q], other = h ? s1 : s0;
+          const nv2 pr = odd ? (nv2){other, mine} : (nv2){mine, other};
+          __builtin_nontemporal_store(pr, reinterpret_cast<nv2*>(obase + (int64_t)(16 * rb + 4 * q + lg) * p.ldo + c));
+        }
+      } else {
+        for (int q = 0; q < 4; ++q)
+          __builtin_nontemporal_store(v[q], obase + (int64_t)(16 * rb + 4 * q + lg) * p.ldo + 16 * cb + lr);
+      }
+    }
 }
 
 __global__ void maxdiff_k(const double* a, const double* b, int64_t n, double* out) {
@@ -250,6 +286,10 @@ int main(int argc, char** argv) {
                                 dim3((nt / ROWS) * (n / COLS)), dim3(256), 0, 0, v); }, bsf, NAME); \
   if (!SO) check(NAME);
   VAR(128, 128, 2, true, "store-only 128x128");
+  time([&] { hipLaunchKernelGGL(store_mfma_layout<false>, dim3((nt / 128) * (n / 128)), dim3(256), 0, 0, v); },
+       bsf, "store-only mfma layout (4 x 128 B)");
+  time([&] { hipLaunchKernelGGL(store_mfma_layout<true>, dim3((nt / 128) * (n / 128)), dim3(256), 0, 0, v); },
+       bsf, "store-only mfma layout, pairs (2 x 256 B)");
   VAR(128, 128, 2, false, "variant 128x128 unroll 2 (=lib)");
   VAR(128, 128, 4, false, "variant 128x128 unroll 4");
   VAR(128, 64, 2, false, "variant 64 rows x 128");
