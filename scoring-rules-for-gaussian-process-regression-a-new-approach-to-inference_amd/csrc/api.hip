@@ -2205,7 +2205,7 @@ int fitc_syrk(gps_ctx* ctx, const double* kscale, const double* base, double* ds
   p.M = (int)mp; p.N = (int)mp; p.K = (int)ctx->fn_pad; p.kscale = kscale;
   p.lower_out = 1; p.ksplit = ks;
   if (int rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p)) return rc;
-  Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1) * mp * mp);
+  Prof pr(ctx, "syrk_slab_sum", 0, 8.0 * (ks + 1 + (base ? 1 : 0)) * mp * mp);
   if (packed)
     HIPCHK(launch_sym_pack(ctx->slabB.d(), mp * mp, ks, 0, (int)ctx->m, (int)mp, dst, ctx->stream));
   else
@@ -2431,10 +2431,11 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   }
   if (bside) HIPCHK(hipEventRecord(ctx->b_join, ctx->aux[1]));
   // B_p = Kmnᵀ Λ⁻¹ Knm (lower tiles, split-K slabs); sharded: packed and all-reduced with b,
-  // Σlogλ, Σy²/λ, in row blocks overlapped with the SYRK (ctx->ar_chunks)
+  // Σlogλ, Σy²/λ, in row blocks overlapped with the SYRK (ctx->ar_chunks); one
+  // rank: the slab sum adds K̃mm and writes B = K̃mm + Σ slabs straight into Am (one launch)
   if (shard) {
     if ((rc = fitc_syrk_allreduce(ctx, red, blen, mp + 2))) return rc;
-  } else if ((rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, Bacc, false))) {
+  } else if ((rc = fitc_syrk(ctx, ctx->ilam.d(), ctx->Kmm.d(), ctx->Am.d(), false))) {
     if (bside) (void)hipStreamWaitEvent(s, ctx->b_join, 0);
     return rc;
   }
@@ -2442,10 +2443,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
     if ((rc = fitc_test_prepass(ctx))) return rc;
   // --- B = K̃mm + Σ_p B_p, factor redundantly on every rank
-  if (shard)
-    HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
-  else
-    HIPCHK(launch_sym_slab_sum(Bacc, 0, 1, (int)mp, ctx->Kmm.d(), ctx->Am.d(), s));
+  if (shard) HIPCHK(launch_sym_unpack(Bacc, (int)m, (int)mp, ctx->Kmm.d(), 0, ctx->Am.d(), s));
   // (the r pass's column tiles [0, qn1), like q's, as soon as the top-level Lb11⁻¹ is final)
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;

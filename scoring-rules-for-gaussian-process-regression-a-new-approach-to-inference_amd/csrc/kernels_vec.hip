@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256) void sym_slab_sum_kernel(const double* __restr
   const int i = (int)(e / M), j = (int)(e - (int64_t)i * M);
   double v = 0.0;
   if (j / GPS_TILE <= i / GPS_TILE) {
-    if (base) v = base[e];
     for (int q = 0; q < nslab; ++q) v += slab[(int64_t)q * stride + e];
+    if (base) v = base[e] + v;  // base + (Σ slabs): the sum, then the base, as two launches would
   }
   dst[e] = v;
 }
