@@ -2372,10 +2372,12 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   int rc;
   if ((rc = reset_info(ctx))) return rc;
   // --- replicated m×m part: K̃mm = K(Z,Z) + 1e-3 I (KF:36), Lm⁻¹
+  // (built into Am, the factorisation's input, which it overwrites; the copy kept for B's base
+  //  and the gradients is a second build on aux[0] beside the factorisation when that stream is
+  //  in use — the same kernel on the same inputs, so the same bits — else a copy here)
   if ((rc = gram(ctx, "gram_kmm", ctx->Z.d(), (int)m, ctx->Z.d(), (int)m, ctx->fd, th, 1e-3, 0, 1,
-                 ctx->Kmm.d(), mp, (int)mp, (int)mp)))
+                 ctx->Am.d(), mp, (int)mp, (int)mp)))
     return rc;
-  HIPCHK(hipMemcpyAsync(ctx->Am.p, ctx->Kmm.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
   // (a persistent top level has no recursion step to overlap the pre-pass with)
   const bool preq = ctx->pred_pre && mp > GPS_TILE && !dag_block(ctx, mp / GPS_TILE);
   // this shard's rows of K(X, Z): with a pre-pass, first on the main stream (the q column tiles
@@ -2388,6 +2390,11 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
       if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     HIPCHK(hipEventRecord(ctx->kn_fork, s));
     HIPCHK(hipStreamWaitEvent(ctx->aux[0], ctx->kn_fork, 0));
+    if ((rc = gram(ctx, "gram_kmm", ctx->Z.d(), (int)m, ctx->Z.d(), (int)m, ctx->fd, th, 1e-3, 0,
+                   1, ctx->Kmm.d(), mp, (int)mp, (int)mp, ctx->aux[0])))
+      return rc;
+  } else {
+    HIPCHK(hipMemcpyAsync(ctx->Kmm.p, ctx->Am.p, (size_t)mp * mp * 8, hipMemcpyDeviceToDevice, s));
   }
   if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
                  ctx->Knm.d(), mp, (int)np, (int)mp, kside ? ctx->aux[0] : nullptr)))
