@@ -295,10 +295,13 @@ __device__ __forceinline__ void gram_stage_half(const double* __restrict__ src, 
                                                 const double* __restrict__ cen, double (&v)[D / 2]) {
   const int t = threadIdx.x, gi = base + (t >> 1), k0 = (t & 1) * (D / 2);
 #pragma unroll
-  for (int k = 0; k < D / 2; ++k)
-    v[k] = gi < rows_real ? src[(int64_t)gi * D + k0 + k] * inv_ell[k0 + k] -
-                                cen[k0 + k] * inv_ell[k0 + k]
+  for (int k = 0; k < D / 2; ++k) {
+    // (a non-finite centre coordinate is replaced by 0 — the same shift for both sides, so
+    //  still exact — lest one bad input row poison its whole tile instead of its own row)
+    const double c = cen[k0 + k] * inv_ell[k0 + k];
+    v[k] = gi < rows_real ? src[(int64_t)gi * D + k0 + k] * inv_ell[k0 + k] - (isfinite(c) ? c : 0.0)
                           : 0.0;
+  }
 }
 template <int D>
 __device__ __forceinline__ void gram_put_half(double* xs, double* hs, const double (&v)[D / 2]) {

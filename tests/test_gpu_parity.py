@@ -533,6 +533,33 @@ def test_gram_mfma_offset_data(gpu_ctx, d, n, m, uplo):
 
 
 @pytest.mark.parametrize("d", [8, 16])
+def test_gram_mfma_nan_propagates(gpu_ctx, d):
+    """A NaN length-scale or input reaches the output of the matrix-core kernel (its exp clamp
+    keeps NaN, as the direct-difference kernels do), so a fit on it fails loudly instead of
+    factoring a clamped matrix; a NaN input row poisons its own output row only, also when it
+    is the row its tile is centred on."""
+    from gpscore._lib import GPS_ARD, ptr
+    rng = np.random.default_rng(d)
+    x, xp = rng.standard_normal((300, d)), rng.standard_normal((200, d))
+    ell = np.zeros(d)
+    ell[d // 2] = np.nan
+    out = np.zeros((300, 200))
+    gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), 300, ptr(xp), 200, d, 0.0, ptr(ell), d, 0.0, 0, ptr(out))
+    assert np.all(np.isnan(out))
+    x[17, 3] = np.nan
+    out[:] = 0.0
+    gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), 300, ptr(xp), 200, d, 0.0, ptr(np.zeros(d)), d, 0.0, 0,
+                 ptr(out))
+    assert np.all(np.isnan(out[17])) and np.isfinite(np.delete(out, 17, axis=0)).all()
+    x[17, 3] = 0.5
+    x[128, 5] = np.nan  # the first row of a tile: the tile's centre
+    out[:] = 0.0
+    gpu_ctx.call("gps_gram", GPS_ARD, ptr(x), 300, ptr(xp), 200, d, 0.0, ptr(np.zeros(d)), d, 0.0, 0,
+                 ptr(out))
+    assert np.all(np.isnan(out[128])) and np.isfinite(np.delete(out, 128, axis=0)).all()
+
+
+@pytest.mark.parametrize("d", [8, 16])
 def test_gram_mfma_lower_persistent(gpu_ctx, d):
     """A lower build large enough for the persistent grid (n = 11 648: 91 tile rows, 4186 lower
     tiles, several per workgroup, row changes inside a workgroup's run) with the diagonal add:
