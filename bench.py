@@ -426,6 +426,20 @@ C5_FIXTURE = os.path.join(ROOT, "tests", "golden", "c5_n1_outputs.json")
 FITC_VECS = ("loo_mu", "loo_var", "pred_mu", "pred_var")
 
 
+def rccl_identity(ctl, glib):
+    """Which RCCL every rank runs (gps_rccl_info): ncclGetVersion and the file that holds
+    ncclAllReduce.  torch is imported before libgpscore in this process (the gloo control plane),
+    so the library's librccl.so.1 and libamdhip64 resolve to torch's bundled copies — one HIP
+    runtime per process — rather than /opt/rocm's."""
+    v, path = glib.rccl_info()
+    per = ctl.gather([v, path])
+    return {"version": v, "version_str": "%d.%d.%d" % (v // 10000, v // 100 % 100, v % 100),
+            "path": path, "all_ranks_same": all(p == per[0] for p in per),
+            "why": "torch (imported first for the gloo control plane) bundles librccl.so with "
+                   "SONAME librccl.so.1; the library's DT_NEEDED librccl.so.1 binds to it, as its "
+                   "libamdhip64 binds to torch's bundled HIP runtime"}
+
+
 def comm_check(ctl, world, rank, local, info, kind="rccl"):
     """Every rank's communicator as the library reports it (gps_comm_info: RCCL's own
     ncclCommCount / ncclCommUserRank), gathered over the control plane: the run's ranks agree
@@ -438,6 +452,38 @@ def comm_check(ctl, world, rank, local, info, kind="rccl"):
     return {"ranks_seen": sorted({n for _, _, n, _, _ in seen}), "all_ranks_agree": bool(agree),
             "per_rank": [{"rank": r, "local_rank": lr, "comm_count": n, "comm_user_rank": ur,
                           "kind": k} for r, lr, n, ur, k in seen]}
+
+
+# SURVEY.md §8e / DESIGN §8: the FITC unit's main-stream phases (gps_phase_enable) grouped by what
+# scales with the ranks.  replicated: K̃mm + Lm's factorisation, B's unpack + Lb's, c = B⁻¹b;
+# sharded: Knm, the q / r row norms with λ and the LOO terms, B's SYRK; exposed exchange: the main
+# stream's wait for B's last chunked all-reduce and the scalar all-reduce; the rest of the unit
+# (predict with its score sums) is what the unit time leaves.
+SPLIT = {"replicated": ("kmm_lm", "lb", "c"), "sharded": ("knm", "q", "syrk", "r"),
+         "exposed_exchange": ("exchange", "scal")}
+
+
+def scaling_split(ph, steps, world, ms_unit):
+    """Per-unit ms of each group of phases and the all-reduce record of one rank: B's exchange
+    (the all-reduces of >= 64 KiB: its row blocks, b and the two scalars ride in the last) with
+    its bytes per unit and the ring bus rate 2(N−1)/N · bytes / time (NCCL's busbw convention;
+    each all-reduce timed on its own stream, so the time includes any wait for the slowest
+    rank), and the small ones (score / LOO scalars)."""
+    pm = {k: v["ms"] / steps for k, v in ph.get("phases", {}).items()}
+    out = {"phases_ms": pm}
+    for g, names in SPLIT.items():
+        out[g + "_ms"] = sum(pm.get(k, 0.0) for k in names)
+    out["predict_and_rest_ms"] = ms_unit - sum(pm.values()) if pm else None
+    big = [(b, ms) for b, ms in ph.get("allreduce", []) if b >= 65536]
+    small = [(b, ms) for b, ms in ph.get("allreduce", []) if b < 65536]
+    b_bytes = sum(b for b, _ in big) / steps
+    b_ms = sum(ms for _, ms in big) / steps
+    out["allreduce_B"] = {"count": len(big) / steps, "bytes": b_bytes, "ms": b_ms,
+                          "bus_GBps": (2.0 * (world - 1) / world * b_bytes / (b_ms * 1e-3) / 1e9)
+                          if b_ms > 0 and world > 1 else None}
+    out["allreduce_small"] = {"count": len(small) / steps,
+                              "ms": sum(ms for _, ms in small) / steps}
+    return out
 
 
 def sample_indices(n):
@@ -706,12 +752,20 @@ def main():
         bad = os.environ.get("GPS_BENCH_DRY_COMM_COUNT", "")
         n_seen = int(bad.split(":")[1]) if bad and bad.split(":")[0] == str(rank) else world
         rc = comm_check(ctl, world, rank, local, (n_seen, rank, "dry"), kind="dry")
+        from gpscore import _lib as glib  # (loads the library; gps_rccl_info needs no device)
+        rc["library"] = rccl_identity(ctl, glib)
+        # the N > 1 scaling split on a stand-in phase record (no GPU): the same code and schema
+        stand_in = {"phases": {k: {"count": 1, "ms": 1.0} for g in SPLIT.values() for k in g},
+                    "allreduce": [[8.0 * 4000 * 4001 / 2 / 4, 1.0]] * 4 + [[16.0, 0.05]]}
+        split = scaling_split(stand_in, 1, world, 20.0)
         if rank == 0:
             ok = sorted(r for r, _, _ in everyone) == list(range(world)) and \
                 len({p for _, _, p in everyone}) == world
             line = {"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
                     "ranks": everyone, "ranks_ok": ok, "steps": args.steps,
-                    "warmup": args.warmup, "fitc": {"rccl": rc}}
+                    "warmup": args.warmup,
+                    "fitc": {"rccl": rc, "C5": {"scaling_split": {"per_rank": [split] * world,
+                                                                  "max_over_ranks": split}}}}
             if not rc["all_ranks_agree"]:
                 line["failures"] = [f"communicators disagree with --gpus {world}"]
             print(json.dumps(line))
@@ -858,6 +912,7 @@ def main():
                 fitc["error"] = comm_err or "gps_comm_init failed on another rank"
             else:
                 fitc["rccl"] = comm_check(ctl, world, rank, local, info)
+                fitc["rccl"]["library"] = rccl_identity(ctl, gpscore._lib)
                 if not fitc["rccl"]["all_ranks_agree"]:
                     failures.append(f"RCCL communicators disagree with --gpus {world}: "
                                     f"{fitc['rccl']['per_rank']}")
@@ -879,6 +934,14 @@ def main():
             for _ in range(args.warmup):
                 funit()
             tf = timed(ctl, ctx, funit, args.steps)
+            # the same production schedule with phase events (after the headline pass: the
+            # events are not in `value`), every rank's split gathered
+            ctx.phases(True)
+            tph = timed(ctl, ctx, funit, args.steps)
+            ctx.phases(False)
+            split = scaling_split(ctx.phase_collect(), args.steps, world, 1e3 * tph / args.steps)
+            split["unit_ms_with_events"] = 1e3 * tph / args.steps
+            splits = ctl.gather(split)
             fprof, fms_acct = kernel_pass(ctl, ctx, funit, args.steps)
             fphases = phases(ctl, ctx, fgp, thf, args.steps, fprof, 1e3 * tf / args.steps)
             fobj = fgp.fit(theta=thf, return_loo=False).objectives
@@ -896,6 +959,13 @@ def main():
                              args.steps, alg_flop("fitc", fc, world)),
                          "kernel_accounting_ms_per_step": fms_acct,
                          "phases": fphases,
+                         "scaling_split": {
+                             "per_rank": splits,
+                             "max_over_ranks": {k: max(sp[k] for sp in splits)
+                                                for k in splits[0] if k.endswith("_ms") and
+                                                splits[0][k] is not None},
+                             "note": "main-stream phases of the production unit (events on), grouped "
+                                     "replicated / sharded / exposed exchange (bench.SPLIT)"},
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             if fout is not None:
                 if args.write_c5_fixture and world == 1 and rank == 0:

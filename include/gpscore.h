@@ -53,8 +53,9 @@ enum {
 /* ---- context ------------------------------------------------------------ */
 /* ABI version of this header; gps_version() returns the library's.  Bumped whenever an entry
  * point changes its arguments or an array it writes changes size (500: gps_ctx_stats takes a
- * capacity, gps_comm_info and gps_build_id added).  The binding refuses a mismatch at load. */
-#define GPS_ABI_VERSION 500
+ * capacity, gps_comm_info and gps_build_id added; 600: gps_phase_enable / gps_phase_collect /
+ * gps_rccl_info added).  The binding refuses a mismatch at load. */
+#define GPS_ABI_VERSION 600
 int gps_version(void);
 /* The SHA-256 (hex) of the sources the library was built from (csrc/, this header; computed by
  * gpscore/buildid.py at build time).  Writes at most cap-1 characters and a NUL; returns the
@@ -143,6 +144,12 @@ enum {
                              largest upward rank with the round-4 measured task durations, 2 the
                              same with round 3's, 0 earliest estimated start.  Same values bitwise
                              (the order changes only which workgroup runs a task, and when). */
+  GPS_OPT_FITC_DEP = 27,  /* 1 (default): when a FITC m×m factorisation is one persistent launch
+                             (m_pad ≤ 20 tiles), the row norms over its inverse (q = ‖Lm⁻¹k_i‖²,
+                             r = ‖Lb⁻¹k_i‖²) start on a second stream while it runs, each column
+                             tile as soon as its row of L⁻¹ is final (device-side row signals),
+                             and a completion launch after it takes the tiles left; 0: the row
+                             norms after the factorisation.  Same tiles, same values bitwise. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 
@@ -172,6 +179,26 @@ int gps_dag_task_list(int T, int flags, uint32_t* out, int cap);
 int gps_prof_enable(gps_ctx* ctx, int on);
 /* Synchronises, then writes a JSON object {tag: {count, ms, flop, bytes}} and clears. */
 int gps_prof_collect(gps_ctx* ctx, char* json_out, int64_t cap);
+/* Phase timing of the FITC forward on its production schedule (the launches, streams and their
+ * overlap are unchanged; gps_prof_enable instead serialises them): with on, every FITC forward
+ * (gps_fitc_fit, the gradients' and block-LOO's forward) records a timing event on its main
+ * stream at each phase boundary, and two around every all-reduce on the stream that issues it.
+ * Phases, each the main-stream time since the previous mark (K20:222-234 restated):
+ *   "kmm_lm"   K̃mm and Lm's factorisation (replicated on every rank; Knm's Gram beside it),
+ *   "knm"      the wait for Knm (sharded),  "q" the q row norms and λ (sharded),
+ *   "syrk"     B's split-K SYRK with its packing (sharded; the row-block all-reduces beside it),
+ *   "exchange" the main stream's wait for B's last all-reduce (exposed exchange),
+ *   "lb"       B's unpack and Lb's factorisation, "c" c = B⁻¹b (replicated),
+ *   "r"        the r row norms, g and the LOO terms (sharded), "scal" the scalar all-reduce.
+ * gps_phase_collect synchronises and writes {"phases": {name: {"count", "ms"}}, "allreduce":
+ * [[bytes, ms], ...]} (one pair per all-reduce, on its own stream) and clears. */
+int gps_phase_enable(gps_ctx* ctx, int on);
+int gps_phase_collect(gps_ctx* ctx, char* json_out, int64_t cap);
+/* The RCCL this process runs: ncclGetVersion and the file holding ncclAllReduce as the dynamic
+ * linker resolved it (the library links librccl.so.1 from /opt/rocm/lib; a process that loaded a
+ * librccl.so.1 first — torch's bundled copy, when torch is imported before the library — runs
+ * that one).  Writes at most cap-1 characters and a NUL to path; needs no device. */
+int gps_rccl_info(int* version, char* path, int cap);
 
 /* ---- L1 building blocks ---------------------------------------------------- */
 /* ARD(x, xp, a, b) KF:7-23 / rbf SD:8-21: out[n][m] = sf2·exp(−½‖(x−x')/ℓ‖²)

@@ -19,6 +19,7 @@
 //   [L11, L11⁻¹] = rec(A11);  L21 = A21 L11⁻ᵀ;  A22 −= L21 L21ᵀ;
 //   T = L21 L11⁻¹ (into A21);  [L22, L22⁻¹] = rec(A22);  L⁻¹21 = −L22⁻¹ T
 //   → n³/3 (potrf) + n³/3 (trtri) flops; base case: 128×128 LDS kernel.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <string.h>
@@ -78,7 +79,11 @@ struct LocalGroup {
   std::vector<std::vector<double>> in;
   std::vector<double> sum;
   std::vector<char> taken;  // ranks held by a live context (a second context may not join as one)
-  // the device path: one device for every member, ≤ kLocalSumMax ranks
+  int joined = 0;           // ranks that have joined; the reduction path is read only once all n
+                            // have (a rank that summed before a member on another
+                            // device joined would have taken the device path, that member the
+                            // host path, and one generation would have mixed the two)
+  // the device path: one device for every member, ≤ kLocalSumMax ranks (final once joined == n)
   int device = -1;
   bool device_ok = true;
   std::vector<double*> stage;   // per rank, written only by its owner (grown after every reader)
@@ -129,6 +134,9 @@ struct gps_ctx {
   bool dag_fine = true;                // GPS_OPT_DAG_FINE
   int dag_order = 1;                   // GPS_OPT_DAG_ORDER
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
+  bool fitc_dep = true;                // GPS_OPT_FITC_DEP: FITC row norms behind the m×m factorisations
+  int* dag_sig = nullptr;              // the top-level persistent launch's row signals (kSig*), if any
+  DBuf dsig;                           // the FITC signal blocks: Lm's, Lb's (kSigInts ints each)
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2(3T + order) + fine: device task list, length
   // factor buffers (L⁻¹, L) known to hold zeros for a padded size: potrf_inv writes their lower
   // triangles only and refuses a buffer without an entry here (zero_factor); freeing or growing
@@ -160,6 +168,13 @@ struct gps_ctx {
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
   std::vector<ProfRec> recs;
+  // phase timing of the FITC forward on the production schedule (gps_phase_enable)
+  bool phase = false;
+  std::vector<hipEvent_t> ph_ev;
+  size_t ph_used = 0;
+  std::vector<std::pair<std::string, int>> ph_marks;          // (phase, event) on the main stream
+  struct PhAr { double bytes; int e0, e1; };
+  std::vector<PhAr> ph_ar;                                    // one per all-reduce
   // pinned host staging for small results
   double* hsmall = nullptr;
   int* hinfo = nullptr;
@@ -200,6 +215,7 @@ struct gps_ctx {
   hipEvent_t pre_fork = nullptr, pre_join = nullptr, preb_fork = nullptr;
   hipEvent_t kn_fork = nullptr, kn_join = nullptr;  // the FITC Knm Gram beside Lm's factorisation
   hipEvent_t b_fork = nullptr, b_join = nullptr;    // the FITC b pass beside B's SYRK
+  hipEvent_t r_fork = nullptr, r_join = nullptr;    // the FITC r pass behind Lb's factorisation
   DBuf fslab_pre;
   Theta fth;
   // ---- comm: RCCL (gps_comm_init) or the in-process group (gps_comm_init_local)
@@ -337,6 +353,22 @@ struct Prof {
     c->recs.push_back({tag, e0, e1, flop, bytes});
   }
 };
+
+// phase timing (gps_phase_enable): a timing event from the phase pool recorded on st
+int phase_event(gps_ctx* c, hipStream_t st) {
+  if (c->ph_used == c->ph_ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    c->ph_ev.push_back(e);
+  }
+  const int i = (int)c->ph_used++;
+  return hipEventRecord(c->ph_ev[i], st) == hipSuccess ? i : -1;
+}
+void phase_mark(gps_ctx* c, const char* name) {
+  if (!c->phase) return;
+  const int e = phase_event(c, c->stream);
+  if (e >= 0) c->ph_marks.push_back({name, e});
+}
 
 // fork/join event from a per-call pool (reset by potrf_inv)
 hipEvent_t sync_event(gps_ctx* c) {
@@ -479,6 +511,28 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
   return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
 
+// The FITC row norms behind a running m×m factorisation (GPS_OPT_FITC_DEP): output
+// column tiles [0, ncols) of Knm·L⁻ᵀ (L⁻¹ in L, being written by a persistent launch of the
+// context's FITC width whose row signals are sig).  mode 1: the dependent launch (EPI_ROWSQ) —
+// each column tile as soon as its row of L⁻¹ is final; mode 2: the completion launch after the
+// factorisation — the tiles mode 1 left, and with w / dot the last column tile's row dot g = Knm·w
+// (EPI_ROWSQ_DOT, as fitc_fit_core's r pass).  Both write fslab's row-norm partials as
+// fitc_rowsq_cols does, so the sums that read them are unchanged.
+int dag_width(const gps_ctx* ctx, int64_t nb, bool half);
+int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int mode,
+                   hipStream_t st, const double* w = nullptr, double* dot = nullptr) {
+  const int64_t np = ctx->fn_pad, mp = ctx->m_pad;
+  GemmParams p = gp0();
+  p.A = ctx->Knm.d(); p.lda = mp; p.B = L; p.ldb = mp;
+  p.M = (int)np; p.N = (int)ncols; p.K = (int)ncols; p.tri = TRI_K_LE_J;
+  p.kend = (int)pad_to(ctx->m, 16);
+  p.out0 = ctx->fslab.d(); p.ld_out = np;
+  p.dep_sig = sig; p.dep_q = sig + kSigQueue; p.dep_err = static_cast<int*>(ctx->info.p) + 1;
+  p.dep_grid = dag_width(ctx, mp / GPS_TILE, true); p.dep_mode = mode;
+  p.w = w; p.out1 = dot;
+  return gemm(ctx, LAY_N, LAY_T, dot ? EPI_ROWSQ_DOT : EPI_ROWSQ, p, st);
+}
+
 // the task list of an nb-tile persistent block under the context's options
 int dag_list_key(const gps_ctx* ctx, int64_t nb) {
   return (int)(2 * (3 * nb + ctx->dag_order) + (ctx->dag_fine ? 1 : 0));
@@ -498,6 +552,15 @@ void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t
   }
   dag_blocks(ctx, nb / 2, sizes, cnt);
   dag_blocks(ctx, nb - nb / 2, sizes, cnt);
+}
+
+// workgroups of a persistent launch of nb tiles: one per CU, or half the CUs for the FITC m×m
+// factorisations, whose chain needs ~70 workgroups at m = 2048 and whose side streams (the row
+// norms, the test pre-pass) then get the other half (C4 12.72 -> 12.29 ms; the full GP's blocks
+// want every CU: 124.2 vs 126.1 ms, profiles/r3_dag_width_ab.txt)
+int dag_width(const gps_ctx* ctx, int64_t nb, bool half) {
+  const int auto_w = half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
+  return (int)std::min<int64_t>(ctx->dag_wgs > 0 ? ctx->dag_wgs : auto_w, std::max<int64_t>(4, 2 * nb * nb));
 }
 
 // recursive Cholesky + inverse on a padded (multiple of 128) SPD block.
@@ -531,16 +594,11 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     d.cnt = static_cast<int*>(ctx->dag_cnt.p) + ctx->dag_cnt_used;
     d.spin_ticks = 200000000ull;  // 2 s at the 100 MHz real-time clock
     d.group = ctx->dag_group;
+    d.sig = top ? ctx->dag_sig : nullptr;  // (a dependent row-norm launch reads its rows)
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
-    // width: one workgroup per CU, or half the CUs for the FITC m×m factorisations, whose chain
-    // needs ~70 workgroups at m = 2048 and whose side stream (the test pre-pass) then gets the
-    // other half (C4 12.72 -> 12.29 ms; the full GP's blocks want every CU: 124.2 vs 126.1 ms,
-    // profiles/r3_dag_width_ab.txt)
-    const int auto_w = ctx->dag_half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
-    const int nwg = std::min(ctx->dag_wgs > 0 ? ctx->dag_wgs : auto_w, std::max(4, 2 * nb * nb));
-    HIPCHK(launch_potrf_dag(d, nwg, s));
+    HIPCHK(launch_potrf_dag(d, dag_width(ctx, nb, ctx->dag_half), s));
     return 0;
   }
   const int n1b = nb / 2, n2b = nb - n1b;
@@ -713,7 +771,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
       pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
       (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_half,
-      (uintptr_t)ctx->dag_cnt.p, (uintptr_t)ctx->sk_cnt.p};
+      (uintptr_t)ctx->dag_cnt.p, (uintptr_t)ctx->sk_cnt.p, (uintptr_t)ctx->dag_sig};
   for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[dag_list_key(ctx, T)].first.p);  // the task lists
   for (auto& g : ctx->pgraphs)
     if (g.key == key) {
@@ -862,7 +920,16 @@ int group_barrier(gps_ctx* ctx, LocalGroup& G, size_t count) {
 // Σ over the ranks of `count` doubles at buf (device, in place, stream s): ncclAllReduce on
 // the RCCL communicator, or the in-process group's sum (on the device when every member shares
 // one); a no-op on one rank.
+int allreduce_sum_impl(gps_ctx* ctx, double* buf, size_t count, hipStream_t s);
 int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
+  if (!ctx->phase || !sharded(ctx)) return allreduce_sum_impl(ctx, buf, count, s);
+  const int e0 = phase_event(ctx, s);
+  const int rc = allreduce_sum_impl(ctx, buf, count, s);
+  const int e1 = phase_event(ctx, s);
+  if (e0 >= 0 && e1 >= 0) ctx->ph_ar.push_back({8.0 * (double)count, e0, e1});
+  return rc;
+}
+int allreduce_sum_impl(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
   if (ctx->comm) {
     NCCLCHK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, ctx->comm, s));
     return 0;
@@ -870,8 +937,13 @@ int allreduce_sum(gps_ctx* ctx, double* buf, size_t count, hipStream_t s) {
   if (!ctx->lgroup) return 0;
   LocalGroup& G = *ctx->lgroup;
   bool on_device;
-  {
-    std::lock_guard<std::mutex> lk(G.mu);
+  {  // the path is fixed once every rank has joined: wait for the late joiners (as a barrier would)
+    std::unique_lock<std::mutex> lk(G.mu);
+    if (!G.cv.wait_for(lk, std::chrono::seconds(60), [&] { return G.joined == G.n || G.aborted; })) {
+      G.aborted = true;
+      G.cv.notify_all();
+      return fail(ctx, -3, "local all-reduce: timed out waiting for the other ranks to join (group aborted)");
+    }
     if (G.aborted) return fail(ctx, -3, "local all-reduce: another rank left the group");
     on_device = G.device_ok;
   }
@@ -1456,7 +1528,7 @@ static std::vector<DBuf*> ctx_buffers(gps_ctx* ctx) {
                  &ctx->bEf, &ctx->bF, &ctx->ebuf, &ctx->edraws,
                  &ctx->bSg, &ctx->bBf, &ctx->bLf, &ctx->bldf, &ctx->bRem, &ctx->bW, &ctx->bkv,
                  &ctx->bLR, &ctx->bLRv,
-                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->escale, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt};
+                 &ctx->ebuf_aux[0], &ctx->ebuf_aux[1], &ctx->ebuf_aux[2], &ctx->bPIs, &ctx->bRW, &ctx->escale, &ctx->bfv, &ctx->rpart, &ctx->dag_cnt, &ctx->sk_cnt, &ctx->dsig};
 }
 
 extern "C" {
@@ -1510,10 +1582,11 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (DBuf* b : ctx_buffers(ctx)) release(ctx, *b);
   for (auto& kv : ctx->dag_lists) release(ctx, kv.second.first);
   for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ph_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->preb_fork, ctx->kn_fork, ctx->kn_join,
-                       ctx->b_fork, ctx->b_join})
+                       ctx->b_fork, ctx->b_join, ctx->r_fork, ctx->r_join})
     if (e) (void)hipEventDestroy(e);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (hipStream_t l : ctx->aux)
@@ -1591,6 +1664,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->dag_wgs = value;
       return 0;
     case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
+    case GPS_OPT_FITC_DEP: ctx->fitc_dep = value != 0; return 0;
     case GPS_OPT_DAG_ORDER:
       ARGCHK(value >= 0 && value <= 2, "GPS_OPT_DAG_ORDER must be 0, 1 or 2");
       ctx->dag_order = value;
@@ -1638,6 +1712,61 @@ int gps_dag_task_list(int T, int flags, uint32_t* out, int cap) {
                                                  (flags & 1) != 0);
   for (int i = 0; i < cap && i < (int)tl.size(); ++i) out[i] = tl[i];
   return (int)tl.size();
+}
+
+int gps_phase_enable(gps_ctx* ctx, int on) {
+  if (int rc = bind(ctx)) return rc;
+  ctx->phase = on != 0;
+  return 0;
+}
+
+int gps_phase_collect(gps_ctx* ctx, char* json_out, int64_t cap) {
+  if (int rc = bind(ctx)) return rc;
+  HIPCHK(sync_ctx_streams(ctx));
+  std::map<std::string, std::pair<int, double>> agg;
+  std::vector<std::string> order;
+  for (size_t i = 1; i < ctx->ph_marks.size(); ++i) {
+    const auto& m = ctx->ph_marks[i];
+    if (m.first == "start") continue;  // a new forward: no phase ends here
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ph_ev[ctx->ph_marks[i - 1].second], ctx->ph_ev[m.second]));
+    if (!agg.count(m.first)) order.push_back(m.first);
+    agg[m.first].first += 1;
+    agg[m.first].second += ms;
+  }
+  std::string js = "{\"phases\": {";
+  for (size_t i = 0; i < order.size(); ++i) {
+    char buf[160];
+    snprintf(buf, sizeof(buf), "%s\"%s\": {\"count\": %d, \"ms\": %.6f}", i ? ", " : "",
+             order[i].c_str(), agg[order[i]].first, agg[order[i]].second);
+    js += buf;
+  }
+  js += "}, \"allreduce\": [";
+  for (size_t i = 0; i < ctx->ph_ar.size(); ++i) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ph_ev[ctx->ph_ar[i].e0], ctx->ph_ev[ctx->ph_ar[i].e1]));
+    char buf[96];
+    snprintf(buf, sizeof(buf), "%s[%.0f, %.6f]", i ? ", " : "", ctx->ph_ar[i].bytes, ms);
+    js += buf;
+  }
+  js += "]}";
+  ctx->ph_marks.clear();
+  ctx->ph_ar.clear();
+  ctx->ph_used = 0;
+  if (!json_out || cap <= (int64_t)js.size()) return fail(ctx, -1, "json buffer too small");
+  memcpy(json_out, js.c_str(), js.size() + 1);
+  return 0;
+}
+
+int gps_rccl_info(int* version, char* path, int cap) {
+  if (!version || !path || cap < 1) return fail(nullptr, -1, "bad arguments");
+  *version = 0;
+  if (ncclGetVersion(version) != ncclSuccess) return fail(nullptr, -3, "ncclGetVersion failed");
+  Dl_info di;
+  memset(&di, 0, sizeof(di));
+  const char* f = dladdr(reinterpret_cast<void*>(&ncclAllReduce), &di) && di.dli_fname ? di.dli_fname : "";
+  snprintf(path, (size_t)cap, "%s", f);
+  return 0;
 }
 
 int gps_prof_enable(gps_ctx* ctx, int on) {
@@ -2225,8 +2354,11 @@ int fitc_syrk_allreduce(gps_ctx* ctx, double* red, int64_t blen, int64_t tail) {
   const int nch = (int)std::min<int64_t>(std::max(1, ctx->ar_chunks), tm);
   if (nch <= 1) {
     if (int rc = fitc_syrk(ctx, ctx->ilam.d(), nullptr, red, true)) return rc;
+    phase_mark(ctx, "syrk");
     Prof pr(ctx, "allreduce_B", 0, 8.0 * (blen + tail));
-    return allreduce_sum(ctx, red, (size_t)(blen + tail), s);
+    const int rc = allreduce_sum(ctx, red, (size_t)(blen + tail), s);
+    phase_mark(ctx, "exchange");
+    return rc;
   }
   const int ks = fitc_syrk_ks(ctx);
   HIPCHK(ensure(ctx, ctx->slabB, (size_t)ks * mp * mp * 8));
@@ -2258,7 +2390,9 @@ int fitc_syrk_allreduce(gps_ctx* ctx, double* red, int64_t blen, int64_t tail) {
     R0 = R1;
   }
   HIPCHK(hipEventRecord(ctx->ar_ev[nch], cs));
+  phase_mark(ctx, "syrk");
   HIPCHK(hipStreamWaitEvent(s, ctx->ar_ev[nch], 0));
+  phase_mark(ctx, "exchange");
   return 0;
 }
 
@@ -2371,6 +2505,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   double* sm = ctx->small.d();        // [logdet_m/2, logdet_b/2, bᵀc]
   int rc;
   if ((rc = reset_info(ctx))) return rc;
+  phase_mark(ctx, "start");
   // --- replicated m×m part: K̃mm = K(Z,Z) + 1e-3 I (KF:36), Lm⁻¹
   // (built into Am, the factorisation's input, which it overwrites; the copy kept for B's base
   //  and the gradients is a second build on aux[0] beside the factorisation when that stream is
@@ -2385,6 +2520,16 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   // Lm11⁻¹ is final); without one, on aux[0] beside Lm's factorisation, whose persistent blocks
   // leave half the CUs free (it needs only X, Z), joined before the q pass
   const bool kside = !preq && ctx->overlap && !ctx->prof;
+  // one persistent launch per m×m factorisation: the q and r row norms behind it (GPS_OPT_FITC_DEP)
+  const bool dep = kside && ctx->fitc_dep && dag_block(ctx, tm);
+  int* sig_m = nullptr;
+  int* sig_b = nullptr;
+  if (dep) {  // (zeroed, stream-ordered before both launches of each pair)
+    HIPCHK(ensure(ctx, ctx->dsig, 2 * kSigInts * sizeof(int)));
+    sig_m = static_cast<int*>(ctx->dsig.p);
+    sig_b = sig_m + kSigInts;
+    HIPCHK(hipMemsetAsync(ctx->dsig.p, 0, 2 * kSigInts * sizeof(int), s));
+  }
   if (kside) {  // (dedicated events: the factorisation reuses its pool of sync events)
     for (hipEvent_t* e : {&ctx->kn_fork, &ctx->kn_join})
       if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -2399,20 +2544,31 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   if ((rc = gram(ctx, "gram_knm", ctx->fX.d(), (int)n, ctx->Z.d(), (int)m, ctx->fd, th, 0.0, 0, 0,
                  ctx->Knm.d(), mp, (int)np, (int)mp, kside ? ctx->aux[0] : nullptr)))
     return rc;
+  // q_i = ‖Lm⁻¹ k_i‖² behind Lm's factorisation, on aux[0] after Knm (the dependent launch)
+  if (dep && (rc = fitc_rowsq_dep(ctx, ctx->Lm.d(), sig_m, mp, 1, ctx->aux[0]))) {
+    (void)hipStreamWaitEvent(s, ctx->kn_join, 0);
+    return rc;
+  }
   if (kside) HIPCHK(hipEventRecord(ctx->kn_join, ctx->aux[0]));
   const int64_t qn1 = preq ? (mp / GPS_TILE / 2) * GPS_TILE : 0;
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lm.d();
   ctx->dag_half = true;  // (the FITC m×m factorisations: see potrf_inv_rec's width)
+  ctx->dag_sig = sig_m;
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr);
+  ctx->dag_sig = nullptr;
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
+  phase_mark(ctx, "kmm_lm");
   if (kside) HIPCHK(hipStreamWaitEvent(s, ctx->kn_join, 0));  // (before any return: Knm in flight)
   if (rc) return rc;
+  phase_mark(ctx, "knm");
   HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
-  // q_i = ‖Lm⁻¹ k_i‖² (the remaining column tiles)
-  if ((rc = fitc_rowsq_cols(ctx, ctx->Lm.d(), qn1, mp, s))) return rc;
+  // q_i = ‖Lm⁻¹ k_i‖²: the tiles the dependent launch left, or the remaining column tiles
+  if ((rc = dep ? fitc_rowsq_dep(ctx, ctx->Lm.d(), sig_m, mp, 2, s)
+                : fitc_rowsq_cols(ctx, ctx->Lm.d(), qn1, mp, s)))
+    return rc;
   double* part = row_part(ctx, np, 2);
   ARGCHK(part != nullptr, "out of device memory");
   {  // q = Σ of the row-norm partials, fused with Λ (one thread per row, many workgroups)
@@ -2421,6 +2577,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                               th.sn2, ctx->q.d(), ctx->lam.d(), ctx->ilam.d(), ctx->ys.d(), scal,
                               part, s));
   }
+  phase_mark(ctx, "q");
   // b_p = Kmnᵀ Λ⁻¹ y: one rank, an HBM-bound pass on aux[1] beside the SYRK (b is first read
   // by c = B⁻¹b after B's factorisation); sharded, it travels in the all-reduce with B
   const bool bside = !shard && ctx->overlap && !ctx->prof;
@@ -2445,6 +2602,8 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   } else if ((rc = fitc_syrk(ctx, ctx->ilam.d(), ctx->Kmm.d(), ctx->Am.d(), false))) {
     if (bside) (void)hipStreamWaitEvent(s, ctx->b_join, 0);
     return rc;
+  } else {
+    phase_mark(ctx, "syrk");
   }
   if (bside) HIPCHK(hipStreamWaitEvent(s, ctx->b_join, 0));
   if (pre_test && ctx->f_test && ctx->fnt > 0 && ctx->overlap && !ctx->prof)
@@ -2455,11 +2614,26 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lb.d();
+  // the r pass's column tiles [0, T − 1) behind Lb's factorisation, on aux[1] (the last column
+  // tile, whose row dot needs c = B⁻¹b, goes with the completion launch)
+  const bool rdep = dep && tm > 1;
+  if (rdep) {
+    for (hipEvent_t* e : {&ctx->r_fork, &ctx->r_join})
+      if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->r_fork, s));
+    HIPCHK(hipStreamWaitEvent(ctx->aux[1], ctx->r_fork, 0));
+    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp - GPS_TILE, 1, ctx->aux[1]))) return rc;
+    HIPCHK(hipEventRecord(ctx->r_join, ctx->aux[1]));
+  }
   ctx->dag_half = true;
+  ctx->dag_sig = rdep ? sig_b : nullptr;
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr);
+  ctx->dag_sig = nullptr;
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
+  if (rdep) HIPCHK(hipStreamWaitEvent(s, ctx->r_join, 0));  // (before any return: r in flight)
   if (rc) return rc;
+  phase_mark(ctx, "lb");
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
   {  // c = Lb⁻ᵀ Lb⁻¹ b
     Prof pr(ctx, "fitc_c", 0, 0);
@@ -2470,9 +2644,13 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                          nullptr, ctx->fslab.d() + tm * np, s, 32));
     HIPCHK(launch_dot(bvec, ctx->c.d(), (int)mp, sm + 2, s));
   }
+  phase_mark(ctx, "c");
   if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
-  {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation), and
-     // g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
+  if (rdep) {  // r_i = ‖Lb⁻¹ k_i‖²: the tiles the dependent launch left and the last column
+               // tile with its row dot g = Knm c
+    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp, 2, s, ctx->c.d(), ctx->g.d()))) return rc;
+  } else {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation),
+            // and g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d() + qn1 * mp; p.ldb = mp;
     p.M = (int)np; p.N = (int)(mp - qn1); p.K = (int)mp; p.tri = TRI_K_LE_J; p.tri_off = (int)qn1;
@@ -2489,7 +2667,9 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                            (int)n, (int)np, ctx->r.d(), ctx->fmu_loo.d(), ctx->fvar_loo.d(),
                            scal + 2, part, s));
   }
+  phase_mark(ctx, "r");
   if ((rc = allreduce_sum(ctx, scal + 2, 2, s))) return rc;
+  phase_mark(ctx, "scal");
   // the pre-pass reads the test inputs: it is done before this call returns (it finished long
   // before on the timeline — B's factorisation and the r pass came after its launch)
   if (ctx->f_pre) HIPCHK(hipStreamWaitEvent(s, ctx->pre_join, 0));
@@ -3438,6 +3618,7 @@ int gps_comm_init_local(gps_ctx* ctx, int nranks, int rank, long long group) {
     ARGCHK(!G->taken[rank], "local group: another live context already holds this rank");
     G->taken[rank] = 1;
     if (ctx->device != G->device) G->device_ok = false;  // members on two devices: host sums
+    if (++G->joined == G->n) G->cv.notify_all();        // the path is final: release the waiters
   }
   ctx->lgroup = G;
   ctx->nranks = nranks;

@@ -86,7 +86,23 @@ struct GemmParams {
   int sk_alone;              // the launch runs without a concurrent forked product (potrf_inv_rec's
                              // trailing update when nothing is forked beside it): the stream-K
                              // tail fills its last round (GPS_OPT_STREAM_K = 2, the default)
+  // Row norms behind a running persistent factorisation (EPI_ROWSQ*, TRI_K_LE_J, tri_off 0, 128
+  // tiles, no split): column tile j needs row tile j of L⁻¹ only.
+  //   dep_mode 1 (the dependent launch): each workgroup takes the heaviest column tile whose row
+  //     is final (dep_sig[kSigRdy + j]) from the per-XCD queues dep_q, waiting for a row only once
+  //     every workgroup of the factorisation has started (dep_sig[kSigStarted] >= dep_grid: they
+  //     are resident, so the wait cannot starve them); otherwise it leaves the tile to
+  //   dep_mode 2 (the completion launch, stream-ordered after the factorisation): block b is tile
+  //     (b % tiles_m, tiles_n − 1 − b / tiles_m), skipped if the dependent launch took it.
+  const int* dep_sig; int* dep_q; int* dep_err; int dep_grid; int dep_mode;
 };
+// The signal block of a persistent factorisation with a dependent row-norm launch (int words,
+// zeroed before the pair is launched; DagParams::sig, GemmParams::dep_sig / dep_q)
+constexpr int kSigStarted = 0;   // workgroups of the factorisation that have started
+constexpr int kSigRowCnt = 64;   // [64] per row tile of L⁻¹: FIN strips completed
+constexpr int kSigRdy = 128;     // [64] per row tile: 1 once the row of L⁻¹ is final
+constexpr int kSigQueue = 192;   // [8 XCDs][64 column tiles] queue heads of one dependent launch
+constexpr int kSigInts = kSigQueue + 8 * 64;
 
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
 struct GemmPlan { int tile, ksplit; };
@@ -269,6 +285,9 @@ struct DagParams {
   unsigned long long spin_ticks;   // 100 MHz s_memrealtime ticks a dependency wait may take
   unsigned long long* trace = nullptr;  // diagnostics only (tools/dag_bench.cpp): 4 words per slot
   int group = 3;                   // 16-deep operand chunks per load group of a strip task (2..4)
+  int* sig = nullptr;              // row-ready signals for a dependent row-norm launch (kSig*):
+                                   // +1 per started workgroup, row tile i flagged once L⁻¹'s row
+                                   // tile i is final (LEAF(0); the last FIN(i, ·) strip)
 };
 hipError_t launch_potrf_dag(const DagParams& p, int nwg, hipStream_t s);
 std::vector<uint32_t> dag_task_list(int T, int order = 1, bool fine = true);

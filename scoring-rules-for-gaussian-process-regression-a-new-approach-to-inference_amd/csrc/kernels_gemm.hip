@@ -125,6 +125,86 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// Row norms behind a running persistent factorisation (GemmParams::dep_mode).
+// Row tiles are dealt to the 8 XCDs in contiguous bands; the dependent launch's workgroup takes,
+// heaviest first, a column tile whose row of L⁻¹ is final, from its own XCD's band (then the
+// others'), through one agent-scope ticket per (XCD, column).  It waits for a row only while
+// every workgroup of the factorisation is known to have started (they are then resident and the
+// factorisation finishes whatever this launch holds); before that it spins at most ~20 µs and
+// then leaves its tile to the completion launch.  Waits are bounded (2 s without progress, then
+// dep_err = 3) and give up when the factorisation reports an error.  Returns the tile (ti, tj) or
+// false.  (Lane 0 decides; the other lanes wait at the barrier.)
+__device__ __forceinline__ int dep_band0(int tm, int x) { return (int)((int64_t)tm * x / 8); }
+__device__ __forceinline__ int dep_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ bool dep_take(const GemmParams& p, double* smem, int& ti, int& tj) {
+  const int T = p.tiles_n, tm = p.tiles_m;
+  if (p.dep_mode == 2) {  // the completion launch: the tiles the dependent launch left
+    const int b = (int)blockIdx.x;
+    tj = T - 1 - b / tm;
+    ti = b - (b / tm) * tm;
+    if (tj < 0) return false;
+    int x = 7;
+    while (x > 0 && dep_band0(tm, x) > ti) --x;
+    const int len = dep_band0(tm, x + 1) - dep_band0(tm, x);
+    return ti - dep_band0(tm, x) >= min(p.dep_q[x * 64 + tj], len);
+  }
+  int* sh = reinterpret_cast<int*>(smem);
+  if (threadIdx.x == 0) {
+    unsigned int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const int me = (int)(xcc & 7);
+    const int* rdy = p.dep_sig + kSigRdy;
+    int res = -1;
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int seen = -1;
+    unsigned int polls = 0;
+    for (;;) {
+      int nready = 0, first_wait = -1;
+      for (int j = T - 1; j >= 0 && res < 0; --j) {
+        if (!dep_ld(rdy + j)) { first_wait = j; continue; }
+        ++nready;
+        for (int o = 0; o < 8 && res < 0; ++o) {
+          const int x = (me + o) & 7, b0 = dep_band0(tm, x), len = dep_band0(tm, x + 1) - b0;
+          int* q = p.dep_q + x * 64 + j;
+          if (dep_ld(q) >= len) continue;
+          const int r = __hip_atomic_fetch_add(q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (r < len) res = (b0 + r) << 8 | j;
+        }
+      }
+      if (res >= 0 || nready == T) break;  // (all rows final and nothing left: cannot happen)
+      if (dep_ld(p.dep_err) != 0x7f7f7f7f) break;  // the factorisation failed: leave the tile
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (dep_ld(p.dep_sig + kSigStarted) < p.dep_grid) {  // not all resident yet: ≤ 20 µs
+        if (now - t0 > 2000) break;
+      } else {  // wait for the next row (bounded: 2 s without a new row and 1e5 polls)
+        const int s = nready * 64 + first_wait;
+        if (s != seen) {
+          seen = s;
+          t0 = now;
+          polls = 0;
+        } else if (++polls > 100000u && now - t0 > 200000000ull) {
+          __hip_atomic_store(p.dep_err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    // agent-scope acquire: the rows' payload (stored write-through and drained before the
+    // factorisation's arrivals) is visible to the operand loads after the barrier
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    sh[0] = res;
+  }
+  __syncthreads();
+  const int res = __builtin_amdgcn_readfirstlane(sh[0]);
+  __syncthreads();  // (gemm_tile's first LDS stores overwrite sh)
+  if (res < 0) return false;
+  ti = res >> 8;
+  tj = res & 255;
+  return true;
+}
+
 template <int ALAY, int BLAY, int EPI, int TILE>
 __device__ __forceinline__ void gemm_tile(const GemmParams& p, int ti, int tj, int kslice,
                                           double* smem, int kb_o = -1, int ke_o = -1,
@@ -146,6 +226,11 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
     }
   }
   if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
+    if (p.dep_mode) {  // behind a running factorisation (dep_take)
+      int ti, tj;
+      if (dep_take(p, smem, ti, tj)) gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, 0, smem);
+      return;
+    }
     if (p.map_mode == 6) {
       // paired column tiles (row norms over a triangular L⁻¹, work ∝ tj + 1): workgroup (ti, q)
       // runs column tile T−1−q and then q, so every workgroup has the same K, (T + 1)·TILE — the
@@ -868,6 +953,22 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // patch order on the factorisation / predictive TRMMs cost C3 27 %, profiles/r2_map5_ab.txt;
   // maps 3 and 7 for the row norms: profiles/r4_rowsq_map_ab.txt)
   const bool rowsq = epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT;
+  if (q.dep_mode) {  // behind a factorisation: one workgroup per tile, tiles from dep_take
+    if (!rowsq || alay != LAY_N || blay != LAY_T || q.tri != TRI_K_LE_J || q.tri_off != 0 ||
+        tile != 128 || q.ksplit != 1 || q.tiles_n > 64 || !q.dep_sig || !q.dep_q || !q.dep_err ||
+        q.dep_mode > 2 || (q.dep_mode == 1 && epi != EPI_ROWSQ) || q.K != q.N)
+      return hipErrorInvalidValue;
+    q.map_mode = 0;
+    q.prio = 0;
+    q.slab_xcd = 0;
+    q.sk_dp = q.sk_wgs = 0;
+    const dim3 grid((unsigned)(q.tiles_m * q.tiles_n)), block(256);
+    if (epi == EPI_ROWSQ)
+      hipLaunchKernelGGL((gemm_f64_kernel<LAY_N, LAY_T, EPI_ROWSQ, 128>), grid, block, 0, s, q);
+    else
+      hipLaunchKernelGGL((gemm_f64_kernel<LAY_N, LAY_T, EPI_ROWSQ_DOT, 128>), grid, block, 0, s, q);
+    return hipGetLastError();
+  }
   const bool pairable = rowsq && q.tri == TRI_K_LE_J && tile == 128 && q.ksplit == 1;
   if (q.map_mode == 6 && !pairable) q.map_mode = 0;  // (an override of 6 leaves the rest automatic)
   // pairs only with ≥ 4 rounds of the 512 workgroup slots: the uniform grid quantises — C4's

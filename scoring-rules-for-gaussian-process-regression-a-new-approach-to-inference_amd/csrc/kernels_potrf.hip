@@ -742,6 +742,11 @@ __global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(Da
   int inc = 0;                         // the arrival the current task adds to *out
   unsigned long long* trow = nullptr;  // TRACE: the current slot's record
   int ndone = 0;                       // queue slots this workgroup completed
+  // row signal of the current task for a dependent row-norm launch (p.sig): row | need << 8 —
+  // need = the FIN strips of the row (NP per FIN(i, k), k < i), 0 for LEAF(0); −1: none
+  int srow = -1;
+  if (p.sig && tid == 0)
+    __hip_atomic_fetch_add(p.sig + kSigStarted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (;;) {
     if (tid == 0) {
       if constexpr (TRACE) {  // (the previous task's "done" stamp lives here for the same reason)
@@ -749,6 +754,12 @@ __global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(Da
       }
       if (out) __hip_atomic_fetch_add(out, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (out2) __hip_atomic_fetch_add(out2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (srow >= 0) {  // (the strip's stores drained before the barrier, as for the arrivals)
+        const int row = srow & 255, need = srow >> 8;
+        if (need == 0 || __hip_atomic_fetch_add(p.sig + kSigRowCnt + row, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) == need - 1)
+          __hip_atomic_store(p.sig + kSigRdy + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       const int t = __hip_atomic_fetch_add(head, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sh[0] = t < p.ntasks ? p.tasks[t] : 0xffffffffu;
       sh[1] = 0;
@@ -837,6 +848,7 @@ __global__ __launch_bounds__(256, GPS_DAG_WAVES_PER_EU) void potrf_dag_kernel(Da
     }
     const int64_t lda = p.lda, ldl = p.ldl;
     out2 = nullptr;
+    srow = !p.sig ? -1 : type == 4 ? ti | (NP * ti) << 8 : (type == 0 && ti == 0) ? 0 : -1;
     if (type == 0) {
       const int64_t o = (int64_t)128 * ti;
       v4::leaf_body<true>(p.A + o * lda + o, lda, p.Linv + o * ldl + o, ldl,

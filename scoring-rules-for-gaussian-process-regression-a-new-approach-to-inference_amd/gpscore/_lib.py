@@ -14,7 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPSCORE_LIB", os.path.join(_HERE, "libgpscore.so"))
-ABI_VERSION = 500  # include/gpscore.h GPS_ABI_VERSION: the signatures below are this version's
+ABI_VERSION = 600  # include/gpscore.h GPS_ABI_VERSION: the signatures below are this version's
 GPS_N_STATS = 6
 GPS_COMM_NONE, GPS_COMM_RCCL, GPS_COMM_LOCAL = 0, 1, 2
 COMM_KINDS = {GPS_COMM_NONE: "none", GPS_COMM_RCCL: "rccl", GPS_COMM_LOCAL: "local"}
@@ -33,6 +33,7 @@ GPS_OPT_DAG_FINE = 22
 GPS_OPT_GEMM_PRIO = 24
 GPS_OPT_DAG_ORDER = 25
 GPS_OPT_SLAB_XCD = 26
+GPS_OPT_FITC_DEP = 27
 GPS_OPT_FORK_MAX = 14
 GPS_OPT_AR_CHUNKS = 15
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
@@ -59,6 +60,9 @@ SIGNATURES = {
     "gps_dag_task_list": (_c_int, [_c_int, _c_int, _c_vp, _c_int]),
     "gps_prof_enable": (_c_int, [_c_vp, _c_int]),
     "gps_prof_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
+    "gps_phase_enable": (_c_int, [_c_vp, _c_int]),
+    "gps_phase_collect": (_c_int, [_c_vp, _c_cp, _c_i64]),
+    "gps_rccl_info": (_c_int, [ctypes.POINTER(_c_int), _c_cp, _c_int]),
     "gps_gram": (_c_int, [_c_vp, _c_int, _P, _c_i64, _P, _c_i64, _c_int, _c_dbl, _P, _c_int,
                           _c_dbl, _c_int, _P]),
     "gps_potrf": (_c_int, [_c_vp, _c_i64, _P, _c_i64, _P]),
@@ -130,6 +134,17 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def rccl_info():
+    """(ncclGetVersion, the file that holds ncclAllReduce as this process resolved it)."""
+    lib = load()
+    v = _c_int()
+    buf = ctypes.create_string_buffer(4096)
+    rc = lib.gps_rccl_info(ctypes.byref(v), buf, len(buf))
+    if rc != 0:
+        raise GpsError(f"gps_rccl_info failed ({rc})")
+    return v.value, buf.value.decode()
 
 
 def build_id():
@@ -213,6 +228,18 @@ class Context:
         import json
         buf = ctypes.create_string_buffer(1 << 16)
         self.call("gps_prof_collect", buf, len(buf))
+        return json.loads(buf.value.decode())
+
+    def phases(self, on=True):
+        """Phase timing of the FITC forward on its production schedule (gps_phase_enable)."""
+        self.call("gps_phase_enable", 1 if on else 0)
+
+    def phase_collect(self):
+        """{"phases": {name: {count, ms}}, "allreduce": [[bytes, ms], ...]} since the last
+        collect (gps_phase_collect)."""
+        import json
+        buf = ctypes.create_string_buffer(1 << 20)
+        self.call("gps_phase_collect", buf, len(buf))
         return json.loads(buf.value.decode())
 
     def set_overlap(self, on=True):

@@ -51,3 +51,15 @@ def test_no_device_raises_loudly():
     from gpscore import _lib
     with pytest.raises(_lib.GpsError):
         _lib.Context(0)
+
+
+def test_rccl_info_names_the_loaded_rccl():
+    """gps_rccl_info (no device needed): the RCCL version and the file that holds ncclAllReduce
+    as the dynamic linker resolved it for this process — the bench's N > 1 line reports both
+    (which RCCL actually ran).  The binding imports torch first in the test and
+    bench processes, so the answer is either torch's bundled librccl or /opt/rocm's."""
+    from gpscore import _lib
+    v, path = _lib.rccl_info()
+    assert v >= 20000, v  # NCCL_VERSION_CODE: major * 10000 + minor * 100 + patch
+    assert "rccl" in os.path.basename(path), path
+    assert os.path.exists(path), path

@@ -1,7 +1,8 @@
 """bench.py's own launcher (VERDICT r3 "next" 1): `python bench.py --gpus N` with no WORLD_SIZE in
 the environment starts N rank processes itself, which meet over gloo; a WORLD_SIZE that disagrees
 with --gpus is refused; a failing rank makes the whole run fail.  `--dry` stops every rank before
-gpscore is imported, so this runs on the CPU."""
+any device call (it loads libgpscore only for gps_rccl_info, which needs no device), so this runs
+on the CPU."""
 import json
 import os
 import subprocess
@@ -114,3 +115,29 @@ def test_spawner_forwards_sigterm_to_ranks():
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_dry_pins_the_scaling_split_schema():
+    """the N > 1 line explains its scaling — per rank the replicated, sharded
+    and exposed-exchange ms of the FITC unit, B's all-reduce bytes / time / bus rate, and which
+    RCCL each rank runs (version and the file holding ncclAllReduce).  --dry builds the split with
+    the production code (bench.scaling_split) on a stand-in phase record."""
+    r = _run(["--gpus", "2", "--dry"])
+    assert r.returncode == 0, r.stderr
+    (j,) = _json_lines(r.stdout)
+    lib = j["fitc"]["rccl"]["library"]
+    assert lib["version"] >= 20000 and "rccl" in os.path.basename(lib["path"]), lib
+    assert lib["all_ranks_same"] and lib["why"]
+    sp = j["fitc"]["C5"]["scaling_split"]
+    assert len(sp["per_rank"]) == 2
+    one = sp["per_rank"][0]
+    for k in ("replicated_ms", "sharded_ms", "exposed_exchange_ms", "predict_and_rest_ms",
+              "phases_ms", "allreduce_B", "allreduce_small"):
+        assert k in one, k
+    assert one["replicated_ms"] == 3.0 and one["sharded_ms"] == 4.0
+    assert one["exposed_exchange_ms"] == 2.0 and one["predict_and_rest_ms"] == 11.0
+    ab = one["allreduce_B"]
+    assert ab["count"] == 4 and ab["bytes"] == 8.0 * 4000 * 4001 / 2
+    # ring bus rate at N = 2: 2(N−1)/N · bytes / time
+    assert abs(ab["bus_GBps"] - ab["bytes"] / 4e-3 / 1e9) < 1e-9
+    assert sp["max_over_ranks"]["replicated_ms"] == 3.0

@@ -174,6 +174,41 @@ def test_counters_cover_every_dependency(T, seed, fine):
     check(em, A)
 
 
+@pytest.mark.parametrize("fine", [0, 1])
+@pytest.mark.parametrize("T,seed", [(2, 3), (5, 4), (9, 5)])
+def test_row_signals_flag_final_rows(T, seed, fine):
+    """The row signals a dependent row-norm launch reads (DagParams::sig, GPS_OPT_FITC_DEP): the
+    kernel flags row tile i of L⁻¹ final at LEAF(0) (i = 0) or when the NP·i-th FIN(i, ·) strip
+    completes.  Under random threshold-permitted orders, every row is flagged exactly once, and
+    at that moment its tiles X_i0..X_ii already hold their final values (nothing writes them
+    later), so a consumer that waits for the flag reads the finished row."""
+    tl = task_list(T, fine)
+    A = spd(T, 40 + seed)
+    Xr = np.linalg.inv(np.linalg.cholesky(A))
+    em = Emu(A, T)
+    rng = np.random.default_rng(seed)
+    rowcnt, flagged = np.zeros(T, int), []
+    pending = list(tl)
+    while pending:
+        ready = [q for q, t in enumerate(pending) if em.ready(t)]
+        t = pending.pop(int(rng.choice(ready)))
+        em.run(t)
+        typ, i = t[0], t[2]
+        row = None
+        if typ == 0 and i == 0:
+            row = 0
+        elif typ == 4:
+            rowcnt[i] += 1
+            row = i if rowcnt[i] == NP_ * i else None
+        if row is not None:
+            flagged.append(row)
+            got = em.X[row * B:(row + 1) * B, :(row + 1) * B]
+            want = Xr[row * B:(row + 1) * B, :(row + 1) * B]
+            assert np.allclose(np.tril(got, row * B), want, rtol=1e-11, atol=1e-11), row
+    assert sorted(flagged) == list(range(T))
+    check(em, A)
+
+
 @pytest.mark.parametrize("T", [5, 20])
 def test_orders_queue_the_same_tasks(T):
     """The orders differ only in sequence: same strip multiset, and they do differ."""

@@ -93,3 +93,42 @@ def test_fitc_blockloo_rccl_ranks(gpu_ctx, tmp_path, P, nfold, objective):
     X, y, _, _, Z, th = _case(*args)
     _blockloo_check(gpu_ctx, X, y, Z, th, nfold, objective, parts,
                     f"fitc_blockloo_rccl_P{P}_{objective}")
+
+
+def test_c5_full_size_rccl_two_ranks_bench_line(tmp_path):
+    """BASELINE configs[4] (FITC n = 200 000, m = 4000, d = 16) at full size,
+    rows sharded over 2 REAL RCCL ranks on the one GPU, through the bench's own N > 1 path
+    (`bench.py --gpus 2 --one-gpu-rccl`: the launcher, gps_comm_init, B's chunked ncclAllReduce
+    beside the SYRK, the scalar all-reduces).  The line must carry RCCL's own rank counts agreeing
+    on both ranks, the sharded C5 outputs equal to the committed N = 1 fixture
+    (tests/golden/c5_n1_outputs.json) within its stated tolerance, the RCCL each rank ran, and
+    the scaling split (replicated / sharded / exposed exchange, B's bytes and bus rate)."""
+    import json
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--one-gpu-rccl",
+                        "--config", "C2", "--steps", "1", "--warmup", "1", "--no-grad", "--no-block",
+                        "--no-cpu"], env=env, capture_output=True, text=True, timeout=600,
+                       start_new_session=True)
+    lines = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stderr[-3000:])
+    j = lines[0]
+    f = j["fitc"]
+    assert f["rccl"]["all_ranks_agree"] and f["rccl"]["ranks_seen"] == [2], f["rccl"]
+    assert f["rccl"]["library"]["all_ranks_same"], f["rccl"]["library"]
+    c5 = f["C5"]
+    assert c5["config"]["ranks"] == 2 and c5["config"]["n"] == 200000
+    par = c5["parity_vs_n1"]
+    assert par["ok"] and par["max_err"] <= par["tol"], par
+    sp = c5["scaling_split"]
+    assert len(sp["per_rank"]) == 2
+    for one in sp["per_rank"]:
+        ab = one["allreduce_B"]
+        # B lower-packed m(m+1)/2 + b (m_pad) + 2 scalars, 8 bytes each, per unit
+        assert ab["bytes"] == 8.0 * (4000 * 4001 // 2 + 4096 + 2), ab
+        assert ab["bus_GBps"] and ab["bus_GBps"] > 0
+        assert one["replicated_ms"] > 0 and one["sharded_ms"] > 0
+    with open(os.path.join(str(tmp_path), "c5_rccl2.json"), "w") as fh:
+        json.dump(j, fh)

@@ -324,6 +324,44 @@ def test_local_group_reinit_and_duplicate_rank(gpu_ctx):
             c.close()
 
 
+def test_local_group_late_joiner(gpu_ctx):
+    """the reduction path of an in-process group (device sums when every member is on
+    one device, host sums otherwise) is read only once all ranks have joined — a rank that
+    reaches its first all-reduce before a late member has joined waits for it (bounded) instead
+    of fixing the path on a partial membership.  Rank 1 joins 1.5 s after rank 0 starts its fit;
+    both ranks' sharded objectives match the whole fit."""
+    import time
+
+    import gpscore
+    from gpscore.dist import shard_rows
+    X, y, Xt, yt, Z, th = _case(2400, 40, 80, 4, 46)
+    ref = _whole(X, y, Xt, yt, Z, th, False, gpu_ctx)
+    _GROUP[0] += 1
+    key = _GROUP[0]
+    stats = (float(y.mean()), float(y.var(ddof=1)))
+
+    def job(r):
+        ctx = gpscore.Context(0)
+        try:
+            if r == 1:
+                time.sleep(1.5)
+            ctx.call("gps_comm_init_local", 2, r, key)
+            gp = gpscore.GP(ctx=ctx)
+            a, b = shard_rows(len(y), 2, r)
+            gp.set_data(X[a:b], y[a:b], kind="fitc", Z=Z, n_total=len(y), ytr_stats=stats)
+            out = gp.fit(theta=th).objectives
+            ctx.call("gps_comm_destroy")
+            return out
+        finally:
+            ctx.close()
+
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        objs = list(ex.map(job, range(2)))
+    for o in objs:
+        for k in OBJS:
+            assert abs(o[k] - ref["obj"][k]) <= 1e-9 * max(1.0, abs(ref["obj"][k])), k
+
+
 def test_fitc_shards_chunked_allreduce_bitwise(gpu_ctx):
     """GPS_OPT_AR_CHUNKS: B's exchange in row blocks, each all-reduced on the comm stream while
     the next block's SYRK runs, gives the same bits as one all-reduce after the whole

@@ -24,7 +24,7 @@ from gpscore import _lib  # noqa: E402
 
 KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN,
         "graph": _lib.GPS_OPT_GRAPH, "tiny": _lib.GPS_OPT_TINY_GEMM, "pre": _lib.GPS_OPT_PRED_PRE,
-        "dag": _lib.GPS_OPT_DAG, "dagt": _lib.GPS_OPT_DAG_TILES, "forkmax": _lib.GPS_OPT_FORK_MAX, "arch": _lib.GPS_OPT_AR_CHUNKS, "sprio": 16, "dagg": _lib.GPS_OPT_DAG_GROUP, "sk": _lib.GPS_OPT_STREAM_K, "dagwg": _lib.GPS_OPT_DAG_WGS, "fine": _lib.GPS_OPT_DAG_FINE, "prio": _lib.GPS_OPT_GEMM_PRIO, "order": _lib.GPS_OPT_DAG_ORDER, "sxcd": _lib.GPS_OPT_SLAB_XCD}
+        "dag": _lib.GPS_OPT_DAG, "dagt": _lib.GPS_OPT_DAG_TILES, "forkmax": _lib.GPS_OPT_FORK_MAX, "arch": _lib.GPS_OPT_AR_CHUNKS, "sprio": 16, "dagg": _lib.GPS_OPT_DAG_GROUP, "sk": _lib.GPS_OPT_STREAM_K, "dagwg": _lib.GPS_OPT_DAG_WGS, "fine": _lib.GPS_OPT_DAG_FINE, "prio": _lib.GPS_OPT_GEMM_PRIO, "order": _lib.GPS_OPT_DAG_ORDER, "sxcd": _lib.GPS_OPT_SLAB_XCD, "dep": _lib.GPS_OPT_FITC_DEP}
 
 
 def main():
