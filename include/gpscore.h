@@ -271,6 +271,13 @@ int gps_fitc_fit(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N_
 int gps_fitc_grad(gps_ctx* ctx, const double* theta, int n_ell, int objective,
                   double obj[GPS_N_OBJ], double* grad, double* grad_z);
 int gps_fitc_predict(gps_ctx* ctx, double* mu, double* var, double sc[GPS_N_SC]);
+/* Diagnostics: the last FITC forward's device intermediates, unpadded and row-major — Knm (n×m,
+ * this shard's rows), λ (n), Lm⁻¹ and Lb⁻¹ (m×m, lower; the factorisations' inverses of K̃mm =
+ * K(Z, Z) + 1e-3·I and B = K̃mm + KmnΛ⁻¹Knm) and K̃mm (m×m, lower).  Any pointer may be NULL.
+ * (DESIGN §9 feeds them one at a time into the oracle's gradient to find which one carries the
+ * GPU's extra rounding.) */
+int gps_fitc_intermediates(gps_ctx* ctx, double* Knm, double* lam, double* Lm_inv, double* Lb_inv,
+                           double* Kmm);
 
 /* ---- block-LOO objectives -----------------------------
  * nfold-fold (the scripts use 4) block leave-out predictive from the diagonal blocks of

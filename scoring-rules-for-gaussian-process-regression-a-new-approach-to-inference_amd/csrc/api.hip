@@ -134,7 +134,8 @@ struct gps_ctx {
   bool dag_fine = true;                // GPS_OPT_DAG_FINE
   int dag_order = 1;                   // GPS_OPT_DAG_ORDER
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
-  bool fitc_dep = true;                // GPS_OPT_FITC_DEP: FITC row norms behind the m×m factorisations
+  int fitc_dep = 1;                    // GPS_OPT_FITC_DEP: FITC row norms behind the m×m factorisations
+                                       // (1: q behind Lm's; 2: and r behind Lb's, g by a GEMV)
   int* dag_sig = nullptr;              // the top-level persistent launch's row signals (kSig*), if any
   DBuf dsig;                           // the FITC signal blocks: Lm's, Lb's (kSigInts ints each)
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2(3T + order) + fine: device task list, length
@@ -1664,7 +1665,10 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->dag_wgs = value;
       return 0;
     case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
-    case GPS_OPT_FITC_DEP: ctx->fitc_dep = value != 0; return 0;
+    case GPS_OPT_FITC_DEP:
+      ARGCHK(value >= 0 && value <= 2, "GPS_OPT_FITC_DEP must be 0, 1 or 2");
+      ctx->fitc_dep = value;
+      return 0;
     case GPS_OPT_DAG_ORDER:
       ARGCHK(value >= 0 && value <= 2, "GPS_OPT_DAG_ORDER must be 0, 1 or 2");
       ctx->dag_order = value;
@@ -2614,15 +2618,15 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lb.d();
-  // the r pass's column tiles [0, T − 1) behind Lb's factorisation, on aux[1] (the last column
-  // tile, whose row dot needs c = B⁻¹b, goes with the completion launch)
-  const bool rdep = dep && tm > 1;
+  // GPS_OPT_FITC_DEP 2: the r pass behind Lb's factorisation too, on aux[1] (every column tile;
+  // g = Knm c, which needs c = B⁻¹b, then by a GEMV)
+  const bool rdep = dep && ctx->fitc_dep == 2;
   if (rdep) {
     for (hipEvent_t* e : {&ctx->r_fork, &ctx->r_join})
       if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     HIPCHK(hipEventRecord(ctx->r_fork, s));
     HIPCHK(hipStreamWaitEvent(ctx->aux[1], ctx->r_fork, 0));
-    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp - GPS_TILE, 1, ctx->aux[1]))) return rc;
+    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp, 1, ctx->aux[1]))) return rc;
     HIPCHK(hipEventRecord(ctx->r_join, ctx->aux[1]));
   }
   ctx->dag_half = true;
@@ -2631,8 +2635,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->dag_sig = nullptr;
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
-  if (rdep) HIPCHK(hipStreamWaitEvent(s, ctx->r_join, 0));  // (before any return: r in flight)
-  if (rc) return rc;
+  if (rc) {
+    if (rdep) (void)hipStreamWaitEvent(s, ctx->r_join, 0);  // (r in flight)
+    return rc;
+  }
   phase_mark(ctx, "lb");
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
   {  // c = Lb⁻ᵀ Lb⁻¹ b
@@ -2646,9 +2652,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   }
   phase_mark(ctx, "c");
   if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
-  if (rdep) {  // r_i = ‖Lb⁻¹ k_i‖²: the tiles the dependent launch left and the last column
-               // tile with its row dot g = Knm c
-    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp, 2, s, ctx->c.d(), ctx->g.d()))) return rc;
+  if (rdep) {  // g = Knm c (a GEMV beside the dependent r launch's tail), then the r tiles it left
+    HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, ctx->c.d(), ctx->g.d(), (int)np, (int)mp, s));
+    HIPCHK(hipStreamWaitEvent(s, ctx->r_join, 0));
+    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp, 2, s))) return rc;
   } else {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation),
             // and g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
     GemmParams p = gp0();
@@ -3422,6 +3429,26 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
       for (int k = 0; k < d; ++k)
         grad_z[j * d + k] = (z1[j * d + k] + 2.0 * z2[j * d + k]) * th.inv_ell[k];
   }
+  return 0;
+}
+
+int gps_fitc_intermediates(gps_ctx* ctx, double* Knm, double* lam, double* Lm_inv, double* Lb_inv,
+                           double* Kmm) {
+  if (int rc = bind(ctx)) return rc;
+  ARGCHK(ctx->f_fitted, "gps_fitc_fit first");
+  const int64_t n = ctx->fn, m = ctx->m, mp = ctx->m_pad;
+  hipStream_t s = ctx->stream;
+  HIPCHK(hipStreamSynchronize(s));
+  auto rows = [&](const DBuf& b, double* dst, int64_t r) -> hipError_t {
+    return hipMemcpy2DAsync(dst, (size_t)m * 8, b.p, (size_t)mp * 8, (size_t)m * 8, (size_t)r,
+                            hipMemcpyDeviceToHost, s);
+  };
+  if (Knm) HIPCHK(rows(ctx->Knm, Knm, n));
+  if (lam) HIPCHK(hipMemcpyAsync(lam, ctx->lam.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+  if (Lm_inv) HIPCHK(rows(ctx->Lm, Lm_inv, m));
+  if (Lb_inv) HIPCHK(rows(ctx->Lb, Lb_inv, m));
+  if (Kmm) HIPCHK(rows(ctx->Kmm, Kmm, m));
+  HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
 

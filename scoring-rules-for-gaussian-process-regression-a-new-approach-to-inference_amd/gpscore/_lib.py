@@ -87,6 +87,7 @@ SIGNATURES = {
     "gps_fitc_blockloo": (_c_int, [_c_vp, _P, _c_int, _c_int, _c_int, _P, _P, _P, _P]),
     "gps_energy_score": (_c_int, [_c_vp, _P, _P, _c_i64, _P, _c_int, _c_dbl, _P, _P]),
     "gps_fitc_predict": (_c_int, [_c_vp, _P, _P, _P]),
+    "gps_fitc_intermediates": (_c_int, [_c_vp, _P, _P, _P, _P, _P]),
     "gps_full_surface": (_c_int, [_c_vp, _P, _P, _c_i64, _c_int, _c_dbl, _P, _c_i64, _P, _c_i64,
                                   _c_int, _P]),
     "gps_comm_unique_id": (_c_int, [_c_cp]),

@@ -566,6 +566,22 @@ def main(only=None):
         dss1 = float(ns["dss"](T(m).view(-1, 1), T(C), b, T(yv).view(-1, 1)))
     save("es_single", m=m, C=C, y=yv, num_sim=40, draws=dr, es=es1, dss=dss1)
 
+    # ---- K20's own dss (K20:106-111: cov_term.inverse()) beside KF's (KF:103-108: chol_solve) on
+    #      the same Gaussians — a moderately and a badly conditioned covariance (own rng: the
+    #      goldens above are untouched)
+    rng3 = np.random.default_rng(31)
+    cases = {}
+    for tag, b, jit in (("well", 24, 0.5), ("ill", 40, 1e-6)):
+        Mx = rng3.standard_normal((b, b))
+        C = Mx @ Mx.T / b + jit * np.eye(b)
+        m, yv = rng3.standard_normal(b), rng3.standard_normal(b)
+        with torch.no_grad():
+            kf = float(ns["dss"](T(m).view(-1, 1), T(C), b, T(yv).view(-1, 1)))
+            k20 = float(ns["dss_k20"](T(m).view(-1, 1), T(C), b, T(yv).view(-1, 1)))
+        cases.update({f"{tag}_m": m, f"{tag}_C": C, f"{tag}_y": yv, f"{tag}_dss_kf": kf,
+                      f"{tag}_dss_k20": k20})
+    save("dss_k20", **cases)
+
     # ---- contour-plot.R surfaces: n = 20 on CP.R's 50 × 50 grid; a d = 2, n = 100 grid ----
     sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "oracle"))
     import gp_oracle as O  # the CP.R data generator only (x = seq(-6, 6, 20), y ~ MVN + noise)

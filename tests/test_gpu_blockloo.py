@@ -117,6 +117,22 @@ def test_compat_es_dss_vs_golden(gpu_ctx):
     assert abs(dv - float(g["dss"])) <= 1e-10 * max(1.0, abs(float(g["dss"]))), (dv, float(g["dss"]))
 
 
+@pytest.mark.parametrize("tag", ["well", "ill"])
+def test_compat_dss_vs_k20_golden(gpu_ctx, tag):
+    """compat.dss (gps_potrs / gps_potrf on the device) against K20's own dss def (K20:106-111,
+    cov_term.inverse()) and KF's (KF:103-108) from the dss_k20 golden: within the covariance's
+    cond·ε, as the two reference defs differ from each other."""
+    from gpscore import compat
+    g = load_golden("dss_k20")
+    C = g[f"{tag}_C"]
+    b = C.shape[0]
+    dv = compat.dss(g[f"{tag}_m"], C, b, g[f"{tag}_y"])
+    tol = 1e-12 if tag == "well" else 1e-15 * np.linalg.cond(C)
+    for k in ("dss_k20", "dss_kf"):
+        ref = float(g[f"{tag}_{k}"])
+        assert abs(dv - ref) <= tol * abs(ref), (k, dv, ref)
+
+
 def test_es_sgd_train(gp):
     """The KF:663-672 SGD loop on ES through GP.train (3 steps, fresh draws per step from one
     Generator) vs the oracle replaying the same draws."""

@@ -188,3 +188,23 @@ def test_cp_surface_oracle_vs_golden(name):
     out = O.cp_surface(g["x"], g["y"], g["ell"], g["sd"])
     for k in range(4):
         assert nrel(out[k], g["surf"][k]) < 1e-9, (k, nrel(out[k], g["surf"][k]))
+
+
+@pytest.mark.parametrize("tag", ["well", "ill"])
+def test_dss_k20_golden(tag):
+    """K20's own dss (K20:106-111, cov_term.inverse()) and KF's (KF:103-108, chol_solve) from the
+    reference's defs on the same Gaussians: the oracle's Cholesky form matches both — to 1e-13
+    on the moderately conditioned covariance, and within the inverse's cond(C)·ε on the badly
+    conditioned one, where the reference's two defs already differ by that much."""
+    g = load_golden("dss_k20")
+    m, C, y = g[f"{tag}_m"], g[f"{tag}_C"], g[f"{tag}_y"]
+    b = C.shape[0]
+    r = y - m
+    L = np.linalg.cholesky(C)
+    w = np.linalg.solve(L, r)
+    d = 0.5 * b * O.LOG2PI + float(np.sum(np.log(np.diag(L)))) + 0.5 * float(w @ w)
+    kf, k20 = float(g[f"{tag}_dss_kf"]), float(g[f"{tag}_dss_k20"])
+    tol = 1e-13 if tag == "well" else 1e-15 * np.linalg.cond(C)
+    assert abs(d - kf) <= tol * abs(kf)
+    assert abs(d - k20) <= tol * abs(k20)
+    assert abs(kf - k20) <= tol * abs(kf)
