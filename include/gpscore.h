@@ -144,12 +144,12 @@ enum {
                              largest upward rank with the round-4 measured task durations, 2 the
                              same with round 3's, 0 earliest estimated start.  Same values bitwise
                              (the order changes only which workgroup runs a task, and when). */
-  GPS_OPT_FITC_DEP = 27,  /* 1 (default): when a FITC m×m factorisation is one persistent launch
-                             (m_pad ≤ 20 tiles), the row norms over its inverse (q = ‖Lm⁻¹k_i‖²,
-                             r = ‖Lb⁻¹k_i‖²) start on a second stream while it runs, each column
-                             tile as soon as its row of L⁻¹ is final (device-side row signals),
-                             and a completion launch after it takes the tiles left; 0: the row
-                             norms after the factorisation.  Same tiles, same values bitwise. */
+  GPS_OPT_FITC_DEP = 27,  /* 1 (default): when K̃mm's factorisation is one persistent launch (m_pad ≤
+                             20 tiles), the q_i = ‖Lm⁻¹k_i‖² row norms start on a second stream while
+                             it runs, each column tile as soon as its row of Lm⁻¹ is final
+                             (device-side row signals; the factorisation then takes 7/16 of the
+                             CUs), and a completion launch after it takes the tiles left; 0: the
+                             row norms after the factorisation.  Same tiles, same values bitwise. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

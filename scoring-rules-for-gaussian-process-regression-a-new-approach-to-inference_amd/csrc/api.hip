@@ -268,13 +268,12 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
 
 // The FITC row norms behind a running m×m factorisation (GPS_OPT_FITC_DEP): output
 // column tiles [0, ncols) of Knm·L⁻ᵀ (L⁻¹ in L, being written by a persistent launch of the
-// context's FITC width whose row signals are sig).  mode 1: the dependent launch (EPI_ROWSQ) —
-// each column tile as soon as its row of L⁻¹ is final; mode 2: the completion launch after the
-// factorisation — the tiles mode 1 left, and with w / dot the last column tile's row dot g = Knm·w
-// (EPI_ROWSQ_DOT, as fitc_fit_core's r pass).  Both write fslab's row-norm partials as
-// fitc_rowsq_cols does, so the sums that read them are unchanged.
+// context's FITC width whose row signals are sig).  mode 1: the dependent launch — each column tile
+// as soon as its row of L⁻¹ is final; mode 2: the completion launch after the factorisation — the
+// tiles mode 1 left.  Both write fslab's row-norm partials as fitc_rowsq_cols does, so the sums
+// that read them are unchanged.
 int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int mode,
-                   hipStream_t st, const double* w, double* dot) {
+                   hipStream_t st) {
   const int64_t np = ctx->fn_pad, mp = ctx->m_pad;
   GemmParams p = gp0();
   p.A = ctx->Knm.d(); p.lda = mp; p.B = L; p.ldb = mp;
@@ -282,9 +281,8 @@ int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int m
   p.kend = (int)pad_to(ctx->m, 16);
   p.out0 = ctx->fslab.d(); p.ld_out = np;
   p.dep_sig = sig; p.dep_q = sig + kSigQueue; p.dep_err = static_cast<int*>(ctx->info.p) + 1;
-  p.dep_grid = dag_width(ctx, mp / GPS_TILE, true); p.dep_mode = mode;
-  p.w = w; p.out1 = dot;
-  return gemm(ctx, LAY_N, LAY_T, dot ? EPI_ROWSQ_DOT : EPI_ROWSQ, p, st);
+  p.dep_grid = dag_width(ctx, mp / GPS_TILE, true, true); p.dep_mode = mode;
+  return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
 
 // the task list of an nb-tile persistent block under the context's options
@@ -311,9 +309,11 @@ void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t
 // workgroups of a persistent launch of nb tiles: one per CU, or half the CUs for the FITC m×m
 // factorisations, whose chain needs ~70 workgroups at m = 2048 and whose side streams (the row
 // norms, the test pre-pass) then get the other half (C4 12.72 -> 12.29 ms; the full GP's blocks
-// want every CU: 124.2 vs 126.1 ms, profiles/r3_dag_width_ab.txt)
-int dag_width(const gps_ctx* ctx, int64_t nb, bool half) {
-  const int auto_w = half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
+// want every CU: 124.2 vs 126.1 ms, profiles/r3_dag_width_ab.txt); 7/16 of the CUs when a
+// dependent row-norm launch runs beside it (GPS_OPT_FITC_DEP: C4 11.62 -> 11.47 ms, 96: 11.53,
+// 80: 11.65, same box, profiles/r6c_dep_ab_c4.txt)
+int dag_width(const gps_ctx* ctx, int64_t nb, bool half, bool dep) {
+  const int auto_w = dep ? std::max(4, ctx->ncu * 7 / 16) : half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
   return (int)std::min<int64_t>(ctx->dag_wgs > 0 ? ctx->dag_wgs : auto_w, std::max<int64_t>(4, 2 * nb * nb));
 }
 
@@ -352,7 +352,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
-    HIPCHK(launch_potrf_dag(d, dag_width(ctx, nb, ctx->dag_half), s));
+    HIPCHK(launch_potrf_dag(d, dag_width(ctx, nb, ctx->dag_half, d.sig != nullptr), s));
     return 0;
   }
   const int n1b = nb / 2, n2b = nb - n1b;
@@ -714,7 +714,7 @@ int gps_ctx_destroy(gps_ctx* ctx) {
   for (hipEvent_t e : ctx->sync_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ar_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : {ctx->pre_fork, ctx->pre_join, ctx->preb_fork, ctx->kn_fork, ctx->kn_join,
-                       ctx->b_fork, ctx->b_join, ctx->r_fork, ctx->r_join})
+                       ctx->b_fork, ctx->b_join})
     if (e) (void)hipEventDestroy(e);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (hipStream_t l : ctx->aux)
@@ -792,10 +792,7 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ctx->dag_wgs = value;
       return 0;
     case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
-    case GPS_OPT_FITC_DEP:
-      ARGCHK(value >= 0 && value <= 2, "GPS_OPT_FITC_DEP must be 0, 1 or 2");
-      ctx->fitc_dep = value;
-      return 0;
+    case GPS_OPT_FITC_DEP: ctx->fitc_dep = value != 0; return 0;
     case GPS_OPT_DAG_ORDER:
       ARGCHK(value >= 0 && value <= 2, "GPS_OPT_DAG_ORDER must be 0, 1 or 2");
       ctx->dag_order = value;

@@ -830,7 +830,13 @@ int gps_fitc_blockloo(gps_ctx* ctx, const double* theta, int n_ell, int nfold, i
     if ((rc = gemm(ctx, LAY_T, LAY_N, EPI_STORE, p))) return rc;
   }
   const double* remote = nullptr;
-  if (shard) {  // the other ranks' folds: Σ_all S − Σ_local S (m×m; all-reduced once)
+  // the other ranks' folds: Σ_all S − Σ_local S (m×m; all-reduced once).  The S_g are PSD with
+  // comparable norms (folds of equal size), so ‖Σ_local‖ ≈ ‖Σ_all‖/P and the subtraction's
+  // rounding is ε(‖Σ_all‖ + ‖Σ_local‖) ≤ ε·(P + 1)/(P − 1)·‖Σ_remote‖ — 3ε at P = 2, not the
+  // cancellation of nearly equal terms; forming the remote sum without it would take
+  // a P·m² exchange (each rank's slot all-reduced) instead of m².  test_gpu_shards' fold-sharded
+  // block-LOO cases hold the result to the unsharded one within 30× its conditioning floor.
+  if (shard) {
     HIPCHK(ensure(ctx, ctx->bRem, (size_t)mm * 8));
     HIPCHK(launch_fold_sum(ctx->bSg.d(), mm, nfl, -1, nullptr, nullptr, 1.0, ctx->bRem.d(), mm, s));
     if ((rc = allreduce_sum(ctx, ctx->bRem.d(), (size_t)mm, s))) return rc;

@@ -309,12 +309,10 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   // one persistent launch per m×m factorisation: the q and r row norms behind it (GPS_OPT_FITC_DEP)
   const bool dep = kside && ctx->fitc_dep && dag_block(ctx, tm);
   int* sig_m = nullptr;
-  int* sig_b = nullptr;
-  if (dep) {  // (zeroed, stream-ordered before both launches of each pair)
-    HIPCHK(ensure(ctx, ctx->dsig, 2 * kSigInts * sizeof(int)));
+  if (dep) {  // (zeroed, stream-ordered before both launches of the pair)
+    HIPCHK(ensure(ctx, ctx->dsig, kSigInts * sizeof(int)));
     sig_m = static_cast<int*>(ctx->dsig.p);
-    sig_b = sig_m + kSigInts;
-    HIPCHK(hipMemsetAsync(ctx->dsig.p, 0, 2 * kSigInts * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(ctx->dsig.p, 0, kSigInts * sizeof(int), s));
   }
   if (kside) {  // (dedicated events: the factorisation reuses its pool of sync events)
     for (hipEvent_t* e : {&ctx->kn_fork, &ctx->kn_join})
@@ -400,27 +398,14 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lb.d();
-  // GPS_OPT_FITC_DEP 2: the r pass behind Lb's factorisation too, on aux[1] (every column tile;
-  // g = Knm c, which needs c = B⁻¹b, then by a GEMV)
-  const bool rdep = dep && ctx->fitc_dep == 2;
-  if (rdep) {
-    for (hipEvent_t* e : {&ctx->r_fork, &ctx->r_join})
-      if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(ctx->r_fork, s));
-    HIPCHK(hipStreamWaitEvent(ctx->aux[1], ctx->r_fork, 0));
-    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp, 1, ctx->aux[1]))) return rc;
-    HIPCHK(hipEventRecord(ctx->r_join, ctx->aux[1]));
-  }
+  // (the r pass behind Lb's factorisation as well — every column tile on aux[1], g = Knm c by a GEMV
+  //  after c — measured no faster: C4 11.84 vs 11.80 ms, profiles/r6b_fitc_dep_ab_c4.txt; the CUs
+  //  Lb's factorisation leaves already run the test-side q* norms)
   ctx->dag_half = true;
-  ctx->dag_sig = rdep ? sig_b : nullptr;
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr);
-  ctx->dag_sig = nullptr;
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
-  if (rc) {
-    if (rdep) (void)hipStreamWaitEvent(s, ctx->r_join, 0);  // (r in flight)
-    return rc;
-  }
+  if (rc) return rc;
   phase_mark(ctx, "lb");
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));
   {  // c = Lb⁻ᵀ Lb⁻¹ b
@@ -434,11 +419,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   }
   phase_mark(ctx, "c");
   if (ctx->f_pre && (rc = fitc_test_prepass_b(ctx))) return rc;
-  if (rdep) {  // g = Knm c (a GEMV beside the dependent r launch's tail), then the r tiles it left
-    HIPCHK(launch_gemv_full(ctx->Knm.d(), mp, ctx->c.d(), ctx->g.d(), (int)np, (int)mp, s));
-    HIPCHK(hipStreamWaitEvent(s, ctx->r_join, 0));
-    if ((rc = fitc_rowsq_dep(ctx, ctx->Lb.d(), sig_b, mp, 2, s))) return rc;
-  } else {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation),
+  {  // r_i = ‖Lb⁻¹ k_i‖² (the column tiles [qn1, mp): the rest came with B's factorisation),
             // and g = Knm c from the same pass over Knm (its last column tile spans the whole K range)
     GemmParams p = gp0();
     p.A = ctx->Knm.d(); p.lda = mp; p.B = ctx->Lb.d() + qn1 * mp; p.ldb = mp;

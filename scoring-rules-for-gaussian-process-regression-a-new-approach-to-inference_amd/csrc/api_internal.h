@@ -124,10 +124,9 @@ struct gps_ctx {
   bool dag_fine = true;                // GPS_OPT_DAG_FINE
   int dag_order = 1;                   // GPS_OPT_DAG_ORDER
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
-  int fitc_dep = 1;                    // GPS_OPT_FITC_DEP: FITC row norms behind the m×m factorisations
-                                       // (1: q behind Lm's; 2: and r behind Lb's, g by a GEMV)
+  bool fitc_dep = true;                // GPS_OPT_FITC_DEP: the q row norms behind Lm's factorisation
   int* dag_sig = nullptr;              // the top-level persistent launch's row signals (kSig*), if any
-  DBuf dsig;                           // the FITC signal blocks: Lm's, Lb's (kSigInts ints each)
+  DBuf dsig;                           // the FITC signal block of Lm's factorisation (kSigInts ints)
   std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2(3T + order) + fine: device task list, length
   // factor buffers (L⁻¹, L) known to hold zeros for a padded size: potrf_inv writes their lower
   // triangles only and refuses a buffer without an entry here (zero_factor); freeing or growing
@@ -206,7 +205,6 @@ struct gps_ctx {
   hipEvent_t pre_fork = nullptr, pre_join = nullptr, preb_fork = nullptr;
   hipEvent_t kn_fork = nullptr, kn_join = nullptr;  // the FITC Knm Gram beside Lm's factorisation
   hipEvent_t b_fork = nullptr, b_join = nullptr;    // the FITC b pass beside B's SYRK
-  hipEvent_t r_fork = nullptr, r_join = nullptr;    // the FITC r pass behind Lb's factorisation
   DBuf fslab_pre;
   Theta fth;
   // ---- comm: RCCL (gps_comm_init) or the in-process group (gps_comm_init_local)
@@ -287,11 +285,11 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
 int pred_rows(gps_ctx* ctx, int64_t r0, int64_t r1, const double* w, hipStream_t st);
 int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipStream_t st);
 int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int mode,
-                   hipStream_t st, const double* w = nullptr, double* dot = nullptr);
+                   hipStream_t st);
 int dag_list_key(const gps_ctx* ctx, int64_t nb);
 bool dag_block(const gps_ctx* ctx, int64_t nb);
 void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t& cnt);
-int dag_width(const gps_ctx* ctx, int64_t nb, bool half);
+int dag_width(const gps_ctx* ctx, int64_t nb, bool half, bool dep);
 int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
                   int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
                   int64_t ldlo, bool top = false);

@@ -86,7 +86,7 @@ struct GemmParams {
   int sk_alone;              // the launch runs without a concurrent forked product (potrf_inv_rec's
                              // trailing update when nothing is forked beside it): the stream-K
                              // tail fills its last round (GPS_OPT_STREAM_K = 2, the default)
-  // Row norms behind a running persistent factorisation (EPI_ROWSQ*, TRI_K_LE_J, tri_off 0, 128
+  // Row norms behind a running persistent factorisation (EPI_ROWSQ, TRI_K_LE_J, tri_off 0, 128
   // tiles, no split): column tile j needs row tile j of L⁻¹ only.
   //   dep_mode 1 (the dependent launch): each workgroup takes the heaviest column tile whose row
   //     is final (dep_sig[kSigRdy + j]) from the per-XCD queues dep_q, waiting for a row only once
@@ -107,8 +107,11 @@ constexpr int kSigInts = kSigQueue + 8 * 64;
 // launch shape chosen for a GEMM (tile edge, K slices); exposed for the microbenchmark
 struct GemmPlan { int tile, ksplit; };
 GemmPlan gemm_plan(int epi, const GemmParams& p, int64_t ws_cap_doubles);
-extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel; 2: and
-                         //    rectangular d = 16 builds the matrix-core kernel
+extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resident kernel; 2 (the
+                         //    default): d in {8, 16} builds of every shape (square lower ones such
+                         //    as K_ff and K̃mm included) on the matrix-core kernel — equal to 1
+                         //    within the centred expansion's rounding, not bitwise (so K̃mm's
+                         //    diagonal tiles are not bitwise symmetric there); d = 1 as in 1
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 extern int g_stream_k;   // stream-K tail of uniform-K 128-tile launches (launch_gemm): 0 never,
                          // 1 every eligible launch, 2 (default) those marked sk_alone

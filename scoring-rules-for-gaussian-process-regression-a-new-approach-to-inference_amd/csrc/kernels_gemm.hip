@@ -225,12 +225,14 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p) {
       return;
     }
   }
-  if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
+  if constexpr (EPI == EPI_ROWSQ) {
     if (p.dep_mode) {  // behind a running factorisation (dep_take)
       int ti, tj;
       if (dep_take(p, smem, ti, tj)) gemm_tile<ALAY, BLAY, EPI, TILE>(p, ti, tj, 0, smem);
       return;
     }
+  }
+  if constexpr (EPI == EPI_ROWSQ || EPI == EPI_ROWSQ_DOT) {
     if (p.map_mode == 6) {
       // paired column tiles (row norms over a triangular L⁻¹, work ∝ tj + 1): workgroup (ti, q)
       // runs column tile T−1−q and then q, so every workgroup has the same K, (T + 1)·TILE — the
@@ -954,19 +956,16 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   // maps 3 and 7 for the row norms: profiles/r4_rowsq_map_ab.txt)
   const bool rowsq = epi == EPI_ROWSQ || epi == EPI_ROWSQ_DOT;
   if (q.dep_mode) {  // behind a factorisation: one workgroup per tile, tiles from dep_take
-    if (!rowsq || alay != LAY_N || blay != LAY_T || q.tri != TRI_K_LE_J || q.tri_off != 0 ||
+    if (epi != EPI_ROWSQ || alay != LAY_N || blay != LAY_T || q.tri != TRI_K_LE_J || q.tri_off != 0 ||
         tile != 128 || q.ksplit != 1 || q.tiles_n > 64 || !q.dep_sig || !q.dep_q || !q.dep_err ||
-        q.dep_mode > 2 || (q.dep_mode == 1 && epi != EPI_ROWSQ) || q.K != q.N)
+        q.dep_mode > 2 || q.K != q.N)
       return hipErrorInvalidValue;
     q.map_mode = 0;
     q.prio = 0;
     q.slab_xcd = 0;
     q.sk_dp = q.sk_wgs = 0;
     const dim3 grid((unsigned)(q.tiles_m * q.tiles_n)), block(256);
-    if (epi == EPI_ROWSQ)
-      hipLaunchKernelGGL((gemm_f64_kernel<LAY_N, LAY_T, EPI_ROWSQ, 128>), grid, block, 0, s, q);
-    else
-      hipLaunchKernelGGL((gemm_f64_kernel<LAY_N, LAY_T, EPI_ROWSQ_DOT, 128>), grid, block, 0, s, q);
+    hipLaunchKernelGGL((gemm_f64_kernel<LAY_N, LAY_T, EPI_ROWSQ, 128>), grid, block, 0, s, q);
     return hipGetLastError();
   }
   const bool pairable = rowsq && q.tri == TRI_K_LE_J && tile == 128 && q.ksplit == 1;

@@ -15,11 +15,15 @@
 // reads only the lower triangle).  Rows >= n / columns >= m are padding: they
 // get 0, or 1 on the diagonal when pad_identity is set, so the padded SPD
 // matrix is diag(A, I) and its factor/inverse are diag(L, I) / diag(L⁻¹, I).
+#include <atomic>
+
 #include "gps_internal.h"
 
 #include <type_traits>
 
 namespace gps {
+
+constexpr int kGramDevs = 64;  // devices the persistent Gram grid-size cache covers
 
 // 16-byte non-temporal store of an output pair (each element is written once and next read by
 // another launch): C3 K_ff 0.387 -> 0.36 ms against plain stores (profiles/r4_gram_ab.txt)
@@ -464,16 +468,20 @@ hipError_t launch_gram(const GramParams& p, hipStream_t s) {
     // persistent over one resident wave of the grid (as many workgroups as fit on every CU at
     // once); a build of fewer than 4 such waves of tiles runs one tile per workgroup instead
     // (2-3 tiles per workgroup would leave the last round a third full: C5 K*m)
-    static int slots[2] = {0, 0};
-    int& sl = slots[p.d == 16];
+    // (cached per device and d: host threads driving contexts on different devices launch
+    //  concurrently — ADVICE r5 — so the cache is atomic and keyed by the current device)
+    static std::atomic<int> slots[kGramDevs][2];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kGramDevs) return hipErrorInvalidValue;
+    int sl = slots[dev][p.d == 16].load(std::memory_order_relaxed);
     if (!sl) {
-      int dev = 0, cus = 0, per = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      int cus = 0, per = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || cus < 1 ||
           per < 1)
         return hipErrorInvalidValue;
       sl = cus * per;
+      slots[dev][p.d == 16].store(sl, std::memory_order_relaxed);
     }
     const int64_t g = items < 4 * (int64_t)sl ? items : sl;
     GramParams q = p;

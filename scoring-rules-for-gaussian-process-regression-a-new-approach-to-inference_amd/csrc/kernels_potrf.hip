@@ -138,10 +138,15 @@ __device__ __forceinline__ void factor_panel(double (&P)[2][16], int p, int lane
   for (int j = 0; j < 16; ++j) {
     const int J = J0 + j;
     const double d = rl(P[DS][j], J & 63);
-    // v_rsq_f64 (~1e-8 relative) + one Newton step; d <= 0 or NaN gives a NaN L_jj (and NaN
-    // below it), which is what the non-PD check after the loop looks for
+    // v_rsq_f64 (~1e-8 relative) + one Newton step leaves 1/√d ~3 ulp off (1.5e0² + the step's
+    // roundings); a second, residual-corrected step (h = 1 − d·r² by FMA, r += r·h/2) brings it to
+    // ~1 ulp, as LAPACK's sqrt and reciprocal.  Round 6: the one-step pivots made the FITC B
+    // factor's inverse 3-10x less accurate than LAPACK's at cond(B) 7e7.  d <= 0 or
+    // NaN gives a NaN L_jj (and NaN below it), which is what the non-PD check after the loop
+    // looks for
     const double y = __builtin_amdgcn_rsq(d);
-    const double rs = y * fma(-0.5 * d * y, y, 1.5);
+    const double r1 = y * fma(-0.5 * d * y, y, 1.5);
+    const double rs = fma(0.5 * r1, fma(-d * r1, r1, 1.0), r1);
     const double ljj = d * rs;
 #pragma unroll
     for (int s = LO ? 0 : 1; s < 2; ++s) {

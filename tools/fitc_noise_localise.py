@@ -9,7 +9,7 @@ m = 40, d = 4, KC over 4 folds, θ- and Z-gradient; K20:655-720).
    unchanged; λ is recomputed from a substituted Knm / Lm⁻¹ unless λ itself is substituted): how
    far the gradient moves from the oracle's own.  The intermediate whose substitution moves it by
    the GPU's excess over the oracle floor is the one to fix.
-Prints a JSON record.  Usage (GPU): python tools/fitc_noise_localise.py [out.json]
+Prints a JSON record.  Usage (GPU): python tools/fitc_noise_localise.py [out.json [intermediates.npz]]
 """
 import json
 import math
@@ -123,6 +123,41 @@ for names in (("Kmm",), ("Lm_inv",), ("Knm",), ("lam",), ("Lb_inv",), ("Kmm", "K
     sub["+".join(names)] = {"grad_vs_oracle": nrel(r[1], o0[1]), "gradZ_vs_oracle": nrel(r[2], o0[2]),
                             "grad_vs_gpu": nrel(r[1], g0[1])}
 rec["substituted"] = sub
+
+# 4. the floor itself: at 1e-15-perturbed inputs, how far each GPU intermediate moves from its value
+#    at the base inputs (GPU) against the oracle's own intermediate's move, and whether the oracle
+#    fed the GPU's perturbed Lb⁻¹ alone reproduces the GPU's perturbed gradient
+save = {"Knm": KnmG, "lam": lamG, "Lm_inv": LmG, "Lb_inv": LbG, "Kmm": KmmG}
+moves = []
+for seed in (1, 2):
+    rng = np.random.default_rng(seed)
+    Xp = X * (1 + 1e-15 * rng.standard_normal(X.shape))
+    Zp = Z * (1 + 1e-15 * rng.standard_normal(Z.shape))
+    gp_ = gpu(Xp, Zp)
+    K2, l2, Lm2, Lb2, Km2 = (np.zeros_like(a) for a in (KnmG, lamG, LmG, LbG, KmmG))
+    gp.ctx.call("gps_fitc_intermediates", P(K2), P(l2), P(Lm2), P(Lb2), P(Km2))
+    KmmO2, LmO2, _ = O.fitc_shared(Zp, th[0], th[1])
+    partO2 = O.fitc_partials(Xp, y, Zp, LmO2, *th)
+    LbO2, _, _ = O.fitc_finish_shared(KmmO2, partO2["B"], partO2["b"])
+    mv = {"gpu": {"Lm_inv": nrel(np.tril(Lm2), np.tril(LmG)), "lam": nrel(l2, lamG),
+                  "Lb_inv": nrel(np.tril(Lb2), np.tril(LbG)), "Knm": nrel(K2, KnmG)},
+          "oracle": {"Lm_inv": nrel(LmO2, LmO), "lam": nrel(partO2["_lam"], partO["_lam"]),
+                     "Lb_inv": nrel(LbO2, LbO), "Knm": nrel(partO2["_Knm"], partO["_Knm"])}}
+    KnmG_b, lamG_b, LmG_b, LbG_b, KmmG_b = KnmG, lamG, LmG, LbG, KmmG
+    KnmG, lamG, LmG, LbG, KmmG = K2, l2, Lm2, Lb2, Km2
+    X_b, Z_b = X, Z
+    X, Z = Xp, Zp
+    r = with_gpu(("Lb_inv",))
+    r_all = with_gpu(("Kmm", "Lm_inv", "Knm", "lam", "Lb_inv"))
+    X, Z = X_b, Z_b
+    KnmG, lamG, LmG, LbG, KmmG = KnmG_b, lamG_b, LmG_b, LbG_b, KmmG_b
+    mv["gpu_perturbed_grad_vs_oracle_with_its_Lb_inv"] = nrel(r[1], gp_[1])
+    mv["gpu_perturbed_grad_vs_oracle_with_all"] = nrel(r_all[1], gp_[1])
+    moves.append(mv)
+    save[f"Lb_inv_p{seed}"] = Lb2
+rec["perturbation_moves"] = moves
+if len(sys.argv) > 2:
+    np.savez_compressed(sys.argv[2], **save)
 out = json.dumps(rec, indent=1)
 print(out)
 if len(sys.argv) > 1:
