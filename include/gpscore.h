@@ -70,7 +70,9 @@ void* gps_ctx_stream(gps_ctx* ctx);
 int gps_ctx_synchronize(gps_ctx* ctx);
 
 /* ---- options ----------------------------------------------------------------
- * Only options the defaults use.  Round-1 experiments measured neutral or slower on C3
+ * Round 6 removed the switches whose other settings had measured slower (4 / 14 fork bounds of
+ * the side-stream product, 16 side-stream priority, 22 unfused chain tasks, 24 GEMM wave-priority
+ * levels); their keys are refused like any unknown key.  Only options the defaults use.  Round-1 experiments measured neutral or slower on C3
  * (lookahead split, CU-reserved streams, in-launch split-K combine, CU-masked main stream,
  * split-K fill of the trailing update) were removed from the library. */
 enum {
@@ -80,8 +82,6 @@ enum {
   GPS_OPT_GEMM_MAP = 3, /* GEMM tile-order override: 0 automatic (default), 1-5 fixed orders, 6 the
                            row norms in paired column tiles (other launches automatic)
                            (A/B measurements; same values bitwise) */
-  GPS_OPT_FORK_MIN = 4, /* smallest recursion block (in 128-row blocks, default 1) whose
-                           off-critical-path product is forked to the side stream */
   GPS_OPT_TINY_GEMM = 7, /* 1 (default): the bottom-of-recursion GEMMs (up to the 1280 level)
                             use the small kernel (16/32-blocks per wave, K split over the waves
                             of a workgroup, no LDS staging, no reduce launch); 0: the 64-tile
@@ -103,14 +103,9 @@ enum {
                             inverted by ONE persistent launch (a device task queue of tile
                             products, per-tile arrival counters); 0: the recursion down to
                             the 128-block leaf.  Same algorithm, other summation order. */
-  GPS_OPT_FORK_MAX = 14, /* largest recursion block (in 128-row blocks) whose off-critical-path
-                            product is forked; 0 (default): no limit */
   GPS_OPT_AR_CHUNKS = 15, /* sharded FITC: B's all-reduce in this many row blocks (default 4),
                              each on a comm stream while the next block's SYRK runs; 1: one
                              all-reduce after the SYRK.  Same bits either way. */
-  GPS_OPT_SIDE_PRIO = 16, /* 1: the side stream (the factorisation's T products) at the lowest
-                             queue priority, so the main stream's launches are dispatched first
-                             as workgroup slots free up; 0 (default): equal priority */
   GPS_OPT_DAG_TILES = 13, /* largest block (in 128-tiles, 2..64, default 20) the persistent
                             factorisation takes */
   GPS_OPT_STREAM_K = 18,  /* the stream-K tail of a 128-tile GEMM launch with uniform K ranges (the
@@ -125,16 +120,6 @@ enum {
                              m×m factorisations (the test pre-pass runs beside them) */
   GPS_OPT_DAG_GROUP = 17, /* persistent factorisation: 16-deep operand chunks a strip task has in
                              flight per load group (2, 3 (default) or 4).  Same values bitwise. */
-  GPS_OPT_DAG_FINE = 22,  /* 1 (default): the persistent factorisation runs the leaf chain's TRSM and
-                             diagonal update as fine parts (16×16 blocks per wave, 8 / 16 workgroups
-                             per tile); 0: as 4 row strips like every other tile task.  Same values
-                             (the strips add exact zero products above X_kk's diagonal). */
-  GPS_OPT_GEMM_PRIO = 24, /* raised wave priority (s_setprio 1) around the GEMM mainloop's MFMA
-                             phase, so that the other workgroup's waves on the SIMD issue their
-                             loads and LDS writes behind it: 1 (default) for the product and
-                             column-reduction launches (C3 −1.1 %), 2 for every launch (the FITC
-                             row-norm and Λ-scaled SYRK launches ran 0.4 % slower), 0 off.  Same
-                             values.  Process-wide. */
   GPS_OPT_SLAB_XCD = 26,  /* 1: split-K GEMM launches (the FITC SYRK, small trailing updates) deal
                              their (tile, K slice) pairs slice-major, each XCD a contiguous run,
                              so one XCD's resident workgroups share a slice's operand rows in its
@@ -169,7 +154,7 @@ int gps_ctx_stats(gps_ctx* ctx, int64_t* out, int cap);
 
 /* Diagnostics: the persistent factorisation's task queue for a block of T tiles (2..64), one
  * word per strip task (type | part << 3 | fine << 7 | i << 8 | j << 16 | k << 24; types 0 LEAF,
- * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN; flags bit 0: the chain tasks' fine parts (GPS_OPT_DAG_FINE),
+ * 1 TRSM, 2 UPD, 3 UPDX, 4 FIN; flags bit 0: the chain tasks' fine parts (the library's queue),
  * bits 2-3: the order (GPS_OPT_DAG_ORDER: 0 or 1 the default 1, 2 order 2, 3 order 0), other
  * bits rejected — kernels_potrf.hip).  Returns the queue length (writes at most cap words);
  * needs no device. */

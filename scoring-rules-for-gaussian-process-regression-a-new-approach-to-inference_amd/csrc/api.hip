@@ -287,7 +287,7 @@ int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int m
 
 // the task list of an nb-tile persistent block under the context's options
 int dag_list_key(const gps_ctx* ctx, int64_t nb) {
-  return (int)(2 * (3 * nb + ctx->dag_order) + (ctx->dag_fine ? 1 : 0));
+  return (int)(3 * nb + ctx->dag_order);
 }
 
 // a block of nb 128-tiles goes to the persistent factorisation (GPS_OPT_DAG)
@@ -373,7 +373,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   if (Lout) HIPCHK(hipMemcpy2DAsync(Lout + (int64_t)n1 * ldlo, ldlo * 8, W, (size_t)n1 * 8,
                                     (size_t)n1 * 8, n2, hipMemcpyDeviceToDevice, s));
   // an event fork + join costs ~13 us of dependent-chain latency (tools/launch_latency.hip)
-  const bool forked = ctx->overlap && n1b >= ctx->fork_min && (!ctx->fork_max || n1b <= ctx->fork_max);
+  const bool forked = ctx->overlap;
   hipStream_t ts = forked ? ctx->side : s;
   hipEvent_t fork = sync_event(ctx), join = sync_event(ctx);
   if (!fork || !join) return fail(ctx, -2, "hipEventCreate failed");
@@ -485,7 +485,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   for (int T : dsizes) {
     const int lk = dag_list_key(ctx, T);
     if (ctx->dag_lists.count(lk)) continue;
-    const std::vector<uint32_t> tl = dag_task_list(T, ctx->dag_order, ctx->dag_fine);
+    const std::vector<uint32_t> tl = dag_task_list(T, ctx->dag_order, true);
     auto& e = ctx->dag_lists[lk];
     HIPCHK(ensure(ctx, e.first, tl.size() * 4));
     // (stream-ordered, never the legacy stream: another context of this process may be
@@ -516,8 +516,8 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
   std::vector<uintptr_t> key = {
       (uintptr_t)A, (uintptr_t)n_pad, (uintptr_t)Linv, (uintptr_t)W, (uintptr_t)logdiag,
       (uintptr_t)nreal, (uintptr_t)Lout, (uintptr_t)ctx->stream, (uintptr_t)ctx->side,
-      (uintptr_t)ctx->overlap, (uintptr_t)ctx->fork_min, (uintptr_t)ctx->fork_max, (uintptr_t)ctx->gemm_map,
-      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)g_gemm_prio, (uintptr_t)g_slab_xcd, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
+      (uintptr_t)ctx->overlap, (uintptr_t)ctx->gemm_map,
+      (uintptr_t)g_tiny_gemm, (uintptr_t)g_stream_k, (uintptr_t)g_slab_xcd, (uintptr_t)ctx->info.p, (uintptr_t)ctx->ws_main.p,
       (uintptr_t)ctx->ws_side.p, (uintptr_t)pre,
       // the pre-pass's operands (only when it is part of the sequence)
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
@@ -750,25 +750,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ARGCHK(value >= 0 && value <= 6, "GPS_OPT_GEMM_MAP must be in 0..6");
       ctx->gemm_map = value;
       return 0;
-    case GPS_OPT_FORK_MIN: ctx->fork_min = value < 1 ? 1 : value; return 0;
-    case GPS_OPT_FORK_MAX: ctx->fork_max = value < 0 ? 0 : value; return 0;
-    case GPS_OPT_SIDE_PRIO: {  // the side stream at the lowest queue priority (or back)
-      if ((value != 0) == ctx->side_low) return 0;
-      int least = 0, greatest = 0;
-      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      // the replacement first: if its creation fails, the context keeps its working side stream
-      // (never the legacy null stream, which would serialise against other contexts' captures)
-      hipStream_t ns = nullptr;
-      if (value) HIPCHK(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, least));
-      else HIPCHK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
-      const hipError_t es = hipStreamSynchronize(ctx->side);
-      if (es != hipSuccess) (void)hipStreamDestroy(ns);
-      HIPCHK(es);
-      (void)hipStreamDestroy(ctx->side);
-      ctx->side = ns;
-      ctx->side_low = value != 0;
-      return 0;
-    }
     case GPS_OPT_AR_CHUNKS:
       ARGCHK(value >= 1 && value <= 64, "GPS_OPT_AR_CHUNKS must be in 1..64");
       ctx->ar_chunks = value;
@@ -779,7 +760,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       g_stream_k = value;
       return 0;
     case GPS_OPT_SLAB_XCD: g_slab_xcd = value != 0; return 0;
-    case GPS_OPT_GEMM_PRIO: g_gemm_prio = value < 0 ? 0 : value > 2 ? 2 : value; return 0;
     case GPS_OPT_GRAM_REG:
       ARGCHK(value >= 0 && value <= 2, "GPS_OPT_GRAM_REG must be 0, 1 or 2");
       g_gram_reg = value;
@@ -791,7 +771,6 @@ int gps_ctx_set_option(gps_ctx* ctx, int key, int value) {
       ARGCHK(value >= 0, "GPS_OPT_DAG_WGS must be >= 0");
       ctx->dag_wgs = value;
       return 0;
-    case GPS_OPT_DAG_FINE: ctx->dag_fine = value != 0; return 0;
     case GPS_OPT_FITC_DEP: ctx->fitc_dep = value != 0; return 0;
     case GPS_OPT_DAG_ORDER:
       ARGCHK(value >= 0 && value <= 2, "GPS_OPT_DAG_ORDER must be 0, 1 or 2");

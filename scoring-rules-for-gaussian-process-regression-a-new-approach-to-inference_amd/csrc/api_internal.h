@@ -105,9 +105,6 @@ struct gps_ctx {
   hipStream_t aux[2] = {nullptr, nullptr};  // two more streams (concurrent energy-score folds)
   bool overlap = true;                 // GPS_OPT_OVERLAP
   int gemm_map = 0;                    // GPS_OPT_GEMM_MAP: tile-order override (A/B measurements)
-  int fork_min = 1;                    // GPS_OPT_FORK_MIN: smallest n1 (in 128-blocks) whose T GEMM
-  int fork_max = 0;                    // GPS_OPT_FORK_MAX: largest such n1 (0: no limit)
-  bool side_low = false;               // GPS_OPT_SIDE_PRIO: side stream at the lowest priority
   int ar_chunks = 4;                   // GPS_OPT_AR_CHUNKS: row blocks of the FITC B all-reduce
   std::vector<hipEvent_t> ar_ev;       // their hand-offs to the comm stream (aux[1])
                                        // goes to the side stream (a fork/join costs ~13 us, but
@@ -121,13 +118,12 @@ struct gps_ctx {
   int dag_tiles = 20;                  // GPS_OPT_DAG_TILES
   int dag_group = 3;                   // GPS_OPT_DAG_GROUP
   int dag_wgs = 0;                     // GPS_OPT_DAG_WGS (0: automatic, see dag_width)
-  bool dag_fine = true;                // GPS_OPT_DAG_FINE
   int dag_order = 1;                   // GPS_OPT_DAG_ORDER
   bool dag_half = false;               // this factorisation leaves half the CUs to a side stream
   bool fitc_dep = true;                // GPS_OPT_FITC_DEP: the q row norms behind Lm's factorisation
   int* dag_sig = nullptr;              // the top-level persistent launch's row signals (kSig*), if any
   DBuf dsig;                           // the FITC signal block of Lm's factorisation (kSigInts ints)
-  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 2(3T + order) + fine: device task list, length
+  std::map<int, std::pair<DBuf, int>> dag_lists;  // per 3T + order: device task list, length
   // factor buffers (L⁻¹, L) known to hold zeros for a padded size: potrf_inv writes their lower
   // triangles only and refuses a buffer without an entry here (zero_factor); freeing or growing
   // a buffer forgets its entries (the zero-upper contract is checked, not assumed)

@@ -75,7 +75,7 @@ struct GemmParams {
   int sk_slots;              // workgroup slots of the chip (2 per CU for the 128-tile kernel)
   // set by launch_gemm for the stream-K tail: tiles [sk_dp, tiles) are split over sk_wgs blocks
   int sk_dp, sk_wgs;
-  int prio;                  // 1: the mainloop's MFMA phase at raised wave priority (g_gemm_prio)
+  int prio;                  // 1: the mainloop's MFMA phase at raised wave priority (launch_gemm)
   int mirror;                // lower_out square launch: also write the strictly-lower 32-tiles'
                              // transposes above the diagonal (a symmetric result, in the split-K
                              // reduction when there is one, else by launch_sym_mirror)
@@ -115,7 +115,6 @@ extern int g_gram_reg;   // 1: d in {1, 8, 16} Gram builds use the register-resi
 extern int g_tiny_gemm;  // 1: the bottom-of-recursion GEMMs use the small kernel (gemm_plan)
 extern int g_stream_k;   // stream-K tail of uniform-K 128-tile launches (launch_gemm): 0 never,
                          // 1 every eligible launch, 2 (default) those marked sk_alone
-extern int g_gemm_prio;  // s_setprio around the mainloop's MFMA phase: 0 off, 1 (default) products, 2 all
 extern int g_slab_xcd;   // split-K launches: each XCD runs whole K slices (GPS_OPT_SLAB_XCD)
 constexpr int kStreamKTiles = 4096;  // tickets per stream-K counter array (GemmParams::sk_cnt)
 

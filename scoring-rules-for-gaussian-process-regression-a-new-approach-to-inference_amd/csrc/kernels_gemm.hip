@@ -833,7 +833,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_sym_kernel(const double* __
 }
 
 int g_tiny_gemm = 1;  // GPS_OPT_TINY_GEMM (process-wide; set through gps_ctx_set_option)
-int g_gemm_prio = 1;  // GPS_OPT_GEMM_PRIO (process-wide): s_setprio around the MFMA phase
 // GPS_OPT_SLAB_XCD (process-wide): split-K launches slice-major per XCD.  The FITC SYRK's L2-fabric
 // bytes 4.48 -> 1.91 GB per C4 launch (7x -> 2.9x its Knm operand), time neutral (C4 11.86 -> 11.83,
 // C3 / C5 within noise: profiles/r4_slab_xcd_ab.txt) — the SYRK is not fabric-bound
@@ -1006,7 +1005,8 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   }
   // raised MFMA-phase priority: 1 = the product / column-reduction launches only (C3 −1.3 %;
   // the FITC row-norm launches and the Λ-scaled SYRK ran 0.4 % slower with it), 2 = every launch
-  q.prio = g_gemm_prio == 2 || (g_gemm_prio == 1 && (epi == EPI_STORE || epi == EPI_COLRED) && !q.kscale);
+  // (GPS_OPT_GEMM_PRIO 0 and 2 measured slower and were removed in round 6: DESIGN §6.31)
+  q.prio = (epi == EPI_STORE || epi == EPI_COLRED) && !q.kscale;
   // slice-major per XCD: split-K launches whose tile index is the plain (or remapped) raster
   q.slab_xcd = g_slab_xcd && q.ksplit > 1 && q.sk_wgs == 0 &&
                (q.map_mode == 0 || q.map_mode == 2) && (q.lower_out || q.tri == TRI_NONE);

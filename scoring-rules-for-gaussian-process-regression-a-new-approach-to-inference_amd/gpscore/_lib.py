@@ -21,7 +21,7 @@ COMM_KINDS = {GPS_COMM_NONE: "none", GPS_COMM_RCCL: "rccl", GPS_COMM_LOCAL: "loc
 
 GPS_ARD, GPS_RBF = 0, 1
 GPS_FULL, GPS_LOWER = 0, 1
-GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_FORK_MIN, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 4, 7, 9
+GPS_OPT_OVERLAP, GPS_OPT_GEMM_MAP, GPS_OPT_TINY_GEMM, GPS_OPT_GRAM_REG = 0, 3, 7, 9
 GPS_OPT_GRAPH = 10
 GPS_OPT_PRED_PRE = 11
 GPS_OPT_DAG = 12
@@ -29,12 +29,9 @@ GPS_OPT_DAG_TILES = 13
 GPS_OPT_DAG_GROUP = 17
 GPS_OPT_STREAM_K = 18
 GPS_OPT_DAG_WGS = 19
-GPS_OPT_DAG_FINE = 22
-GPS_OPT_GEMM_PRIO = 24
 GPS_OPT_DAG_ORDER = 25
 GPS_OPT_SLAB_XCD = 26
 GPS_OPT_FITC_DEP = 27
-GPS_OPT_FORK_MAX = 14
 GPS_OPT_AR_CHUNKS = 15
 OBJ_NAMES = ("nlml", "loo_crps", "loo_logs", "logdet", "quad")
 SURFACE_NAMES = ("loo_crps", "insample_crps", "nlml", "loo_logs")

@@ -950,8 +950,11 @@ def test_gemm_slab_xcd_bitwise(gpu_ctx):
                 np.array(list(r.objectives.values()) + list(rf.objectives.values()))]
 
     base = run()
-    with pytest.raises(gpscore.GpsError):
-        gpu_ctx.call("gps_ctx_set_option", 21, 1)
+    # options removed after measured-slower A/Bs are refused: 21 (GEMM_GLDS, round 5); 4 / 14
+    # (FORK_MIN / FORK_MAX), 16 (SIDE_PRIO), 22 (DAG_FINE), 24 (GEMM_PRIO) in round 6
+    for key in (21, 4, 14, 16, 22, 24):
+        with pytest.raises(gpscore.GpsError):
+            gpu_ctx.call("gps_ctx_set_option", key, 1)
     # GPS_OPT_SLAB_XCD (26): split-K launches dealt slice-major per XCD — only which workgroup
     # runs a (tile, slice) pair changes, the slabs and their ordered sum do not
     try:

@@ -2,9 +2,9 @@
 ~5% in GEMM clocks, so variants must be compared inside one run).
 
   python tools/ab_bench.py --config C3 map=0 map=4 ov=0
-  options: map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP), fork (GPS_OPT_FORK_MIN),
+  options: map (GPS_OPT_GEMM_MAP), ov (GPS_OPT_OVERLAP),
            graph (GPS_OPT_GRAPH), tiny (GPS_OPT_TINY_GEMM),
-           pre (GPS_OPT_PRED_PRE), dag (GPS_OPT_DAG), dagt (GPS_OPT_DAG_TILES), fine (GPS_OPT_DAG_FINE)
+           pre (GPS_OPT_PRED_PRE), dag (GPS_OPT_DAG), dagt (GPS_OPT_DAG_TILES), dep (GPS_OPT_FITC_DEP)
 Variants are interleaved round-robin for --rounds rounds; prints the median ms/unit.
 """
 import argparse
@@ -22,9 +22,9 @@ import bench  # noqa: E402
 import gpscore  # noqa: E402
 from gpscore import _lib  # noqa: E402
 
-KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP, "fork": _lib.GPS_OPT_FORK_MIN,
+KEYS = {"map": _lib.GPS_OPT_GEMM_MAP, "ov": _lib.GPS_OPT_OVERLAP,
         "graph": _lib.GPS_OPT_GRAPH, "tiny": _lib.GPS_OPT_TINY_GEMM, "pre": _lib.GPS_OPT_PRED_PRE,
-        "dag": _lib.GPS_OPT_DAG, "dagt": _lib.GPS_OPT_DAG_TILES, "forkmax": _lib.GPS_OPT_FORK_MAX, "arch": _lib.GPS_OPT_AR_CHUNKS, "sprio": 16, "dagg": _lib.GPS_OPT_DAG_GROUP, "sk": _lib.GPS_OPT_STREAM_K, "dagwg": _lib.GPS_OPT_DAG_WGS, "fine": _lib.GPS_OPT_DAG_FINE, "prio": _lib.GPS_OPT_GEMM_PRIO, "order": _lib.GPS_OPT_DAG_ORDER, "sxcd": _lib.GPS_OPT_SLAB_XCD, "dep": _lib.GPS_OPT_FITC_DEP}
+        "dag": _lib.GPS_OPT_DAG, "dagt": _lib.GPS_OPT_DAG_TILES, "arch": _lib.GPS_OPT_AR_CHUNKS, "dagg": _lib.GPS_OPT_DAG_GROUP, "sk": _lib.GPS_OPT_STREAM_K, "dagwg": _lib.GPS_OPT_DAG_WGS, "order": _lib.GPS_OPT_DAG_ORDER, "sxcd": _lib.GPS_OPT_SLAB_XCD, "dep": _lib.GPS_OPT_FITC_DEP}
 
 
 def main():

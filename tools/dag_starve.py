@@ -1,5 +1,5 @@
 """Per-launch durations of the persistent factorisation in C3 units from a rocprofv3 kernel trace
-(tools/r5q_dag_trace.sh): the last unit's 8 launches, and whether a side-stream GEMM overlapped."""
+(a rocprofv3 --kernel-trace of the C3 unit): the last unit's 8 launches, and whether a side-stream GEMM overlapped."""
 import csv
 import sys
 

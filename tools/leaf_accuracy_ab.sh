@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: the leaf pivot's second (residual-corrected) rsqrt step — persistent 2560-block time
-# (dag_bench, base vs new, interleaved) and the FITC block-LOO gradient floor with each library.
+# A library change against a base build (tools/build_ref_lib.sh + tbin/dag_bench_base): the persistent
+# 2560-block time (dag_bench, interleaved) and the FITC block-LOO gradient floor with each library.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
