@@ -486,6 +486,16 @@ def scaling_split(ph, steps, world, ms_unit):
     return out
 
 
+def split_summary(splits):
+    """The gathered per-rank scaling splits and their maxima over the ranks (the slowest rank sets
+    the strong-scaling step)."""
+    keys = [k for k, v in splits[0].items() if k.endswith("_ms") and isinstance(v, (int, float))]
+    return {"per_rank": splits,
+            "max_over_ranks": {k: max(sp[k] for sp in splits) for k in keys},
+            "note": "main-stream phases of the production unit (events on), grouped replicated / "
+                    "sharded / exposed exchange (bench.SPLIT)"}
+
+
 def sample_indices(n):
     """Global row indices whose values the C5 fixture keeps: 48 evenly spaced rows plus both
     sides of every shard boundary of 2, 4 and 8 ranks (gpscore.dist.shard_rows), where an
@@ -764,8 +774,7 @@ def main():
             line = {"metric": METRIC, "value": None, "n_gpus": world, "dry": True,
                     "ranks": everyone, "ranks_ok": ok, "steps": args.steps,
                     "warmup": args.warmup,
-                    "fitc": {"rccl": rc, "C5": {"scaling_split": {"per_rank": [split] * world,
-                                                                  "max_over_ranks": split}}}}
+                    "fitc": {"rccl": rc, "C5": {"scaling_split": split_summary([split] * world)}}}
             if not rc["all_ranks_agree"]:
                 line["failures"] = [f"communicators disagree with --gpus {world}"]
             print(json.dumps(line))
@@ -959,13 +968,7 @@ def main():
                              args.steps, alg_flop("fitc", fc, world)),
                          "kernel_accounting_ms_per_step": fms_acct,
                          "phases": fphases,
-                         "scaling_split": {
-                             "per_rank": splits,
-                             "max_over_ranks": {k: max(sp[k] for sp in splits)
-                                                for k in splits[0] if k.endswith("_ms") and
-                                                splits[0][k] is not None},
-                             "note": "main-stream phases of the production unit (events on), grouped "
-                                     "replicated / sharded / exposed exchange (bench.SPLIT)"},
+                         "scaling_split": split_summary(splits),
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             if fout is not None:
                 if args.write_c5_fixture and world == 1 and rank == 0:
