@@ -132,9 +132,9 @@ enum {
   GPS_OPT_FITC_DEP = 27,  /* 1 (default): when K̃mm's factorisation is one persistent launch (m_pad ≤
                              20 tiles), the q_i = ‖Lm⁻¹k_i‖² row norms start on a second stream while
                              it runs, each column tile as soon as its row of Lm⁻¹ is final
-                             (device-side row signals; the factorisation then takes 7/16 of the
-                             CUs), and a completion launch after it takes the tiles left; 0: the
-                             row norms after the factorisation.  Same tiles, same values bitwise. */
+                             (device-side row signals), and a completion launch after it takes
+                             the tiles left; 0: the row norms after the factorisation.  Same
+                             tiles, same values bitwise. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

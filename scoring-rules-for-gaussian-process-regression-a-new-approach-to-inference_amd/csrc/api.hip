@@ -281,7 +281,7 @@ int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int m
   p.kend = (int)pad_to(ctx->m, 16);
   p.out0 = ctx->fslab.d(); p.ld_out = np;
   p.dep_sig = sig; p.dep_q = sig + kSigQueue; p.dep_err = static_cast<int*>(ctx->info.p) + 1;
-  p.dep_grid = dag_width(ctx, mp / GPS_TILE, true, true); p.dep_mode = mode;
+  p.dep_grid = dag_width(ctx, mp / GPS_TILE, true); p.dep_mode = mode;
   return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
 
@@ -309,11 +309,11 @@ void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t
 // workgroups of a persistent launch of nb tiles: one per CU, or half the CUs for the FITC m×m
 // factorisations, whose chain needs ~70 workgroups at m = 2048 and whose side streams (the row
 // norms, the test pre-pass) then get the other half (C4 12.72 -> 12.29 ms; the full GP's blocks
-// want every CU: 124.2 vs 126.1 ms, profiles/r3_dag_width_ab.txt); 7/16 of the CUs when a
-// dependent row-norm launch runs beside it (GPS_OPT_FITC_DEP: C4 11.62 -> 11.47 ms, 96: 11.53,
-// 80: 11.65, same box, profiles/r6c_dep_ab_c4.txt)
-int dag_width(const gps_ctx* ctx, int64_t nb, bool half, bool dep) {
-  const int auto_w = dep ? std::max(4, ctx->ncu * 7 / 16) : half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
+// want every CU: 124.2 vs 126.1 ms, profiles/r3_dag_width_ab.txt); with the dependent q launch
+// beside Lm's factorisation (GPS_OPT_FITC_DEP) half stays best within noise: 112 / 96 workgroups
+// measured 11.71 / 11.73 against 11.56 ms (profiles/r6i_fitc_dep_ab_c4_phases.txt)
+int dag_width(const gps_ctx* ctx, int64_t nb, bool half) {
+  const int auto_w = half ? std::max(4, ctx->ncu / 2) : ctx->ncu;
   return (int)std::min<int64_t>(ctx->dag_wgs > 0 ? ctx->dag_wgs : auto_w, std::max<int64_t>(4, 2 * nb * nb));
 }
 
@@ -352,7 +352,7 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
-    HIPCHK(launch_potrf_dag(d, dag_width(ctx, nb, ctx->dag_half, d.sig != nullptr), s));
+    HIPCHK(launch_potrf_dag(d, dag_width(ctx, nb, ctx->dag_half), s));
     return 0;
   }
   const int n1b = nb / 2, n2b = nb - n1b;

@@ -285,7 +285,7 @@ int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int m
 int dag_list_key(const gps_ctx* ctx, int64_t nb);
 bool dag_block(const gps_ctx* ctx, int64_t nb);
 void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t& cnt);
-int dag_width(const gps_ctx* ctx, int64_t nb, bool half, bool dep);
+int dag_width(const gps_ctx* ctx, int64_t nb, bool half);
 int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ldl, double* W,
                   int nb, double* logdiag, int* info, int base, int nreal, double* Lout,
                   int64_t ldlo, bool top = false);

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--block", default=None,
                     help="time block_loo(objective, grad=True) (dss / kc / es; ES: 300 draws)")
+    ap.add_argument("--phases", action="store_true",
+                    help="also one pass per variant and round with gps_phase_enable (FITC forward phases)")
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
     c = bench.CONFIGS[args.config]
@@ -67,9 +69,11 @@ def main():
         variants.append((v, opts))
     unit()
     times = {v: [] for v, _ in variants}
+    phs = {v: [] for v, _ in variants}
+    defaults = {KEYS["dagwg"]: 0}  # options a variant sets and the next one might not (reset first)
     for _ in range(args.rounds):
         for name, opts in variants:
-            for key, val in opts.items():
+            for key, val in {**defaults, **opts}.items():
                 ctx.call("gps_ctx_set_option", key, val)
             unit()
             ctx.synchronize()
@@ -78,10 +82,19 @@ def main():
                 unit()
             ctx.synchronize()
             times[name].append(1e3 * (time.perf_counter() - t0) / args.steps)
+            if args.phases:
+                ctx.phases(True)
+                unit()
+                ctx.phases(False)
+                phs[name].append({k: v["ms"] for k, v in ctx.phase_collect()["phases"].items()})
     for name, _ in variants:
         ts = times[name]
         print("%-24s median %8.2f ms/unit  (all: %s)" % (name, float(np.median(ts)),
                                                         " ".join("%.2f" % t for t in ts)))
+        if phs[name]:
+            keys = phs[name][0].keys()
+            print("    phases (median ms): " + " ".join("%s %.3f" % (k, float(np.median([p[k] for p in phs[name]])))
+                                                   for k in keys))
 
 
 if __name__ == "__main__":
