@@ -486,6 +486,26 @@ def scaling_split(ph, steps, world, ms_unit):
     return out
 
 
+# The kernel-accounting pass's FITC kernel classes that every rank repeats (the m×m work: K̃mm, the
+# two factorisations with their recursion products and trailing SYRKs, B's slab sum / unpack,
+# c = B⁻¹b); everything else scales with the rank's rows; allreduce_B is the exchange.
+REPLICATED_TAGS = ("potrf_dag", "gemm_trmm_l", "gemm_trmm_m", "gemm_trmm_s", "gemm_syrk_m",
+                   "gemm_syrk_s", "gemm_m", "gemm_s", "gram_kmm", "fitc_c", "syrk_slab_sum")
+
+
+def scaling_model(prof, steps, world):
+    """Per-rank kernel time (single stream, hipEvents per launch) split into replicated, sharded
+    and exchange kernels, and the compute-only projection to other rank counts: replicated +
+    sharded·world/N (the exchange is what the N > 1 lines measure: scaling_split.allreduce_B)."""
+    ks = kernel_summary(prof, steps)
+    rep_ms = sum(v["ms"] for k, v in ks.items() if k in REPLICATED_TAGS)
+    ex_ms = sum(v["ms"] for k, v in ks.items() if k.startswith("allreduce"))
+    sh_ms = sum(v["ms"] for k, v in ks.items()) - rep_ms - ex_ms
+    return {"replicated_kernels_ms": rep_ms, "sharded_kernels_ms": sh_ms, "exchange_kernels_ms": ex_ms,
+            "replicated_tags": [k for k in ks if k in REPLICATED_TAGS],
+            "compute_projection_ms": {str(n): rep_ms + sh_ms * world / n for n in (1, 2, 4, 8)}}
+
+
 def split_summary(splits):
     """The gathered per-rank scaling splits and their maxima over the ranks (the slowest rank sets
     the strong-scaling step)."""
@@ -493,7 +513,9 @@ def split_summary(splits):
     return {"per_rank": splits,
             "max_over_ranks": {k: max(sp[k] for sp in splits) for k in keys},
             "note": "main-stream phases of the production unit (events on), grouped replicated / "
-                    "sharded / exposed exchange (bench.SPLIT)"}
+                    "sharded / exposed exchange (bench.SPLIT); with m_pad > 20 tiles (C5) the row "
+                    "norms' pre-pass over the top-level L11^-1 columns runs beside the recursion, "
+                    "inside kmm_lm and lb (scaling_model splits by kernel instead)"}
 
 
 def sample_indices(n):
@@ -969,6 +991,7 @@ def main():
                          "kernel_accounting_ms_per_step": fms_acct,
                          "phases": fphases,
                          "scaling_split": split_summary(splits),
+                         "scaling_model": scaling_model(fprof, args.steps, world),
                          "kernels_per_step": kernel_summary(fprof, args.steps)}
             if fout is not None:
                 if args.write_c5_fixture and world == 1 and rank == 0:

@@ -141,3 +141,19 @@ def test_dry_pins_the_scaling_split_schema():
     # ring bus rate at N = 2: 2(N−1)/N · bytes / time
     assert abs(ab["bus_GBps"] - ab["bytes"] / 4e-3 / 1e9) < 1e-9
     assert sp["max_over_ranks"]["replicated_ms"] == 3.0
+
+
+def test_scaling_model_classes():
+    """bench.scaling_model: the kernel-accounting classes split into replicated (the m×m work every
+    rank repeats), sharded and exchange, and the compute projection replicated + sharded·N0/N."""
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = {"potrf_dag": {"count": 4, "ms": 4.0, "flop": 1.0, "bytes": 0},
+            "gemm_trmm_l": {"count": 6, "ms": 2.0, "flop": 1.0, "bytes": 0},
+            "gemm_rowsq": {"count": 6, "ms": 100.0, "flop": 1.0, "bytes": 0},
+            "gemm_syrk_splitk": {"count": 1, "ms": 50.0, "flop": 1.0, "bytes": 0},
+            "allreduce_B": {"count": 4, "ms": 1.0, "flop": 0, "bytes": 6.4e7}}
+    m = bench.scaling_model(prof, 2, 1)
+    assert m["replicated_kernels_ms"] == 3.0 and m["sharded_kernels_ms"] == 75.0
+    assert m["exchange_kernels_ms"] == 0.5
+    assert m["compute_projection_ms"]["8"] == 3.0 + 75.0 / 8
