@@ -48,9 +48,11 @@ CONFIGS = {
     "C3": dict(n=20000, d=8, nt=5000, seed=3),
     "C4": dict(n=40000, d=8, nt=10000, m=2000, seed=4),
     "C5": dict(n=200000, d=16, nt=10000, m=4000, seed=5),
-    # one rank's share of C5 at N = 8 (rows 25 000, test rows 1 250): the per-rank unit of the
-    # 8-GPU strong-scaling run without the exchange, for single-GPU A/Bs (tools/ab_bench.py)
+    # one rank's share of C5 at N = 8 / 4 / 2 (rows 25 000 / 50 000 / 100 000): the per-rank unit of
+    # the strong-scaling run without the exchange, for single-GPU A/Bs (tools/ab_bench.py)
     "C5r8": dict(n=25000, d=16, nt=1250, m=4000, seed=5),
+    "C5r4": dict(n=50000, d=16, nt=2500, m=4000, seed=5),
+    "C5r2": dict(n=100000, d=16, nt=5000, m=4000, seed=5),
 }
 
 

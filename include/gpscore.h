@@ -133,8 +133,11 @@ enum {
                              20 tiles), the q_i = ‖Lm⁻¹k_i‖² row norms start on a second stream while
                              it runs, each column tile as soon as its row of Lm⁻¹ is final
                              (device-side row signals), and a completion launch after it takes
-                             the tiles left; 0: the row norms after the factorisation.  Same
-                             tiles, same values bitwise. */
+                             the tiles left; with m_pad > 20 tiles (a recursive factorisation)
+                             the same for the q pre-pass over the top-level L11⁻¹ columns when
+                             that block is one persistent launch and the pre-pass ≤ 8192 tiles;
+                             0: the row norms after the factorisation.  Same tiles, same values
+                             bitwise. */
 };
 int gps_ctx_set_option(gps_ctx* ctx, int key, int value);
 

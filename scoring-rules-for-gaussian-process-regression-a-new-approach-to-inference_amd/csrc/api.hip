@@ -267,13 +267,14 @@ int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipS
 }
 
 // The FITC row norms behind a running m×m factorisation (GPS_OPT_FITC_DEP): output
-// column tiles [0, ncols) of Knm·L⁻ᵀ (L⁻¹ in L, being written by a persistent launch of the
-// context's FITC width whose row signals are sig).  mode 1: the dependent launch — each column tile
+// column tiles [0, ncols) of Knm·L⁻ᵀ (L⁻¹ in L, its first nb_dag row tiles being written by a
+// persistent launch of the context's FITC width whose row signals are sig: the whole factorisation
+// (C4) or the top-level L11 block of a recursive one (C5)).  mode 1: the dependent launch — each column tile
 // as soon as its row of L⁻¹ is final; mode 2: the completion launch after the factorisation — the
 // tiles mode 1 left.  Both write fslab's row-norm partials as fitc_rowsq_cols does, so the sums
 // that read them are unchanged.
 int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int mode,
-                   hipStream_t st) {
+                   hipStream_t st, int64_t nb_dag) {
   const int64_t np = ctx->fn_pad, mp = ctx->m_pad;
   GemmParams p = gp0();
   p.A = ctx->Knm.d(); p.lda = mp; p.B = L; p.ldb = mp;
@@ -281,7 +282,7 @@ int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int m
   p.kend = (int)pad_to(ctx->m, 16);
   p.out0 = ctx->fslab.d(); p.ld_out = np;
   p.dep_sig = sig; p.dep_q = sig + kSigQueue; p.dep_err = static_cast<int*>(ctx->info.p) + 1;
-  p.dep_grid = dag_width(ctx, mp / GPS_TILE, true); p.dep_mode = mode;
+  p.dep_grid = dag_width(ctx, nb_dag, true); p.dep_mode = mode;
   return gemm(ctx, LAY_N, LAY_T, EPI_ROWSQ, p, st);
 }
 
@@ -348,7 +349,8 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
     d.cnt = static_cast<int*>(ctx->dag_cnt.p) + ctx->dag_cnt_used;
     d.spin_ticks = 200000000ull;  // 2 s at the 100 MHz real-time clock
     d.group = ctx->dag_group;
-    d.sig = top ? ctx->dag_sig : nullptr;  // (a dependent row-norm launch reads its rows)
+    d.sig = ctx->dag_sig;  // (a dependent row-norm launch reads its rows: the first block only)
+    ctx->dag_sig = nullptr;
     ctx->dag_cnt_used += need;
     const double nn = 128.0 * nb;
     Prof pr(ctx, "potrf_dag", 2.0 * nn * nn * nn / 3.0, 0);
@@ -362,8 +364,23 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   double* Li21 = Linv + (int64_t)n1 * ldl;
   double* Li22 = Li21 + n1;
   int rc;
-  if ((rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo)))
-    return rc;
+  // top level with a pre-pass request whose L11 block is one persistent launch and a signal block
+  // (GPS_OPT_FITC_DEP, C5): the pre-pass's column tiles start beside that launch, each as soon as
+  // its row of L11⁻¹ is final, and a completion launch takes the rest once L11⁻¹ is (below)
+  const bool pre_here = top && ctx->pre.kind == PRE_FITC_Q && ctx->pre.n1 == n1;
+  const bool pre_dep = pre_here && ctx->pre.sig && ctx->overlap && dag_block(ctx, n1b);
+  // (on aux[1]: aux[0] may still hold the test-side pre-pass, FIFO ahead of it)
+  if (pre_dep) {
+    hipEvent_t f = sync_event(ctx);
+    if (!f) return fail(ctx, -2, "hipEventCreate failed");
+    HIPCHK(hipEventRecord(f, s));
+    HIPCHK(hipStreamWaitEvent(ctx->aux[1], f, 0));
+    if ((rc = fitc_rowsq_dep(ctx, Linv, ctx->pre.sig, n1, 1, ctx->aux[1], n1b))) return rc;
+    ctx->dag_sig = ctx->pre.sig;  // (consumed by rec(A11)'s persistent launch)
+  }
+  rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo);
+  ctx->dag_sig = nullptr;
+  if (rc) return rc;
   {  // W = L21 = A21 · L11⁻ᵀ
     GemmParams p = gp0();
     p.A = A21; p.lda = lda; p.B = Linv; p.ldb = ldl; p.C = W; p.ldc = n1;
@@ -399,8 +416,8 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   // top level with a pre-pass request: L11⁻¹ is final now, so the product that needs only its
   // rows (FITC: the q column tiles [0, n1)) runs on aux[0] while rec(A22) — mostly
   // latency-bound launches at m ≤ 4k — runs
-  if (top && ctx->pre.kind == PRE_FITC_Q && ctx->pre.n1 == n1) {
-    hipStream_t ps = ctx->overlap ? ctx->aux[0] : s;
+  if (pre_here) {
+    hipStream_t ps = !ctx->overlap ? s : pre_dep ? ctx->aux[1] : ctx->aux[0];
     if (ps != s) {
       hipEvent_t f = sync_event(ctx);
       ctx->pre.join = sync_event(ctx);
@@ -408,7 +425,9 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
       HIPCHK(hipEventRecord(f, s));
       HIPCHK(hipStreamWaitEvent(ps, f, 0));
     }
-    if ((rc = fitc_rowsq_cols(ctx, Linv, 0, n1, ps))) return rc;
+    if ((rc = pre_dep ? fitc_rowsq_dep(ctx, Linv, ctx->pre.sig, n1, 2, ps, n1b)
+                      : fitc_rowsq_cols(ctx, Linv, 0, n1, ps)))
+      return rc;
     if (ps != s) HIPCHK(hipEventRecord(ctx->pre.join, ps));
   }
   if ((rc = potrf_inv_rec(ctx, A22, lda, Li22, ldl, W + (int64_t)n1 * n2, n2b, logdiag + n1, info,
@@ -522,7 +541,7 @@ int potrf_inv(gps_ctx* ctx, double* A, int64_t n_pad, double* Linv, double* W, d
       // the pre-pass's operands (only when it is part of the sequence)
       pre ? (uintptr_t)ctx->pre.n1 : 0, pre ? (uintptr_t)ctx->aux[0] : 0,
       pre ? (uintptr_t)ctx->Knm.p : 0, pre ? (uintptr_t)ctx->fslab.p : 0,
-      pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0,
+      pre ? (uintptr_t)ctx->fn_pad : 0, pre ? (uintptr_t)ctx->m_pad : 0, pre ? (uintptr_t)ctx->pre.sig : 0,
       (uintptr_t)ctx->dag, (uintptr_t)ctx->dag_tiles, (uintptr_t)ctx->dag_group, (uintptr_t)ctx->dag_wgs, (uintptr_t)ctx->dag_half,
       (uintptr_t)ctx->dag_cnt.p, (uintptr_t)ctx->sk_cnt.p, (uintptr_t)ctx->dag_sig};
   for (int T : dsizes) key.push_back((uintptr_t)ctx->dag_lists[dag_list_key(ctx, T)].first.p);  // the task lists

@@ -308,8 +308,17 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   const bool kside = !preq && ctx->overlap && !ctx->prof;
   // one persistent launch per m×m factorisation: the q and r row norms behind it (GPS_OPT_FITC_DEP)
   const bool dep = kside && ctx->fitc_dep && dag_block(ctx, tm);
+  // a recursive m×m factorisation whose top-level L11 is one persistent launch: the q pre-pass
+  // over L11⁻¹'s columns behind that launch (potrf_inv_rec, C5) when the pre-pass is at most 8192
+  // tiles — about what the CUs beside the launch finish while it runs; a larger one would run
+  // on at the dependent launch's column-by-column rate, below the paired order's.  Measured
+  // (DESIGN §6.49): C5's rows per rank at N = 8 / 4 (3136 / 6256 tiles) 28.88 → 28.76 / 49.01 →
+  // 48.81 ms, at N = 2 / 1 (12 512 / 25 008) 89.38 → 90.51 / 169.8 → 170.7.  Lb's r pre-pass stays
+  // after L11 (dependent: +0.6 ms at N = 8 — the test-side q* norms already hold those CUs)
+  const bool pdep = preq && ctx->fitc_dep && ctx->overlap && !ctx->prof &&
+                    dag_block(ctx, tm / 2) && (np / GPS_TILE) * (tm / 2) <= 8192;
   int* sig_m = nullptr;
-  if (dep) {  // (zeroed, stream-ordered before both launches of the pair)
+  if (dep || pdep) {  // (zeroed, stream-ordered before both launches of the pair)
     HIPCHK(ensure(ctx, ctx->dsig, kSigInts * sizeof(int)));
     sig_m = static_cast<int*>(ctx->dsig.p);
     HIPCHK(hipMemsetAsync(ctx->dsig.p, 0, kSigInts * sizeof(int), s));
@@ -329,7 +338,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
                  ctx->Knm.d(), mp, (int)np, (int)mp, kside ? ctx->aux[0] : nullptr)))
     return rc;
   // q_i = ‖Lm⁻¹ k_i‖² behind Lm's factorisation, on aux[0] after Knm (the dependent launch)
-  if (dep && (rc = fitc_rowsq_dep(ctx, ctx->Lm.d(), sig_m, mp, 1, ctx->aux[0]))) {
+  if (dep && (rc = fitc_rowsq_dep(ctx, ctx->Lm.d(), sig_m, mp, 1, ctx->aux[0], tm))) {
     (void)hipStreamWaitEvent(s, ctx->kn_join, 0);
     return rc;
   }
@@ -338,10 +347,12 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lm.d();
+  ctx->pre.sig = pdep ? sig_m : nullptr;
   ctx->dag_half = true;  // (the FITC m×m factorisations: see potrf_inv_rec's width)
-  ctx->dag_sig = sig_m;
+  ctx->dag_sig = dep ? sig_m : nullptr;
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lm.d(), ctx->W.d(), ctx->ldm.d(), (int)m, nullptr);
   ctx->dag_sig = nullptr;
+  ctx->pre.sig = nullptr;
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
   phase_mark(ctx, "kmm_lm");
@@ -350,7 +361,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   phase_mark(ctx, "knm");
   HIPCHK(launch_dot(ctx->ldm.d(), nullptr, (int)mp, sm + 0, s));
   // q_i = ‖Lm⁻¹ k_i‖²: the tiles the dependent launch left, or the remaining column tiles
-  if ((rc = dep ? fitc_rowsq_dep(ctx, ctx->Lm.d(), sig_m, mp, 2, s)
+  if ((rc = dep ? fitc_rowsq_dep(ctx, ctx->Lm.d(), sig_m, mp, 2, s, tm)
                 : fitc_rowsq_cols(ctx, ctx->Lm.d(), qn1, mp, s)))
     return rc;
   double* part = row_part(ctx, np, 2);
@@ -405,6 +416,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   rc = potrf_inv(ctx, ctx->Am.d(), mp, ctx->Lb.d(), ctx->W.d(), ctx->ldb.d(), (int)m, nullptr);
   ctx->dag_half = false;
   ctx->pre.kind = PRE_NONE;
+  ctx->pre.sig = nullptr;
   if (rc) return rc;
   phase_mark(ctx, "lb");
   HIPCHK(launch_dot(ctx->ldb.d(), nullptr, (int)mp, sm + 1, s));

@@ -136,6 +136,8 @@ struct gps_ctx {
     int64_t n1 = 0;
     const double* L = nullptr;         // the top-level L⁻¹
     hipEvent_t join = nullptr;         // waited by the top-level call before it returns
+    int* sig = nullptr;                // row signals: the pre-pass runs behind the L11 block
+                                       // (GPS_OPT_FITC_DEP; zeroed by the caller)
   } pre;
   struct PotrfGraph {                  // one captured potrf_inv launch sequence
     std::vector<uintptr_t> key;
@@ -281,7 +283,7 @@ int gram(gps_ctx* ctx, const char* tag, const double* x, int n, const double* xp
 int pred_rows(gps_ctx* ctx, int64_t r0, int64_t r1, const double* w, hipStream_t st);
 int fitc_rowsq_cols(gps_ctx* ctx, const double* Lx, int64_t c0, int64_t c1, hipStream_t st);
 int fitc_rowsq_dep(gps_ctx* ctx, const double* L, int* sig, int64_t ncols, int mode,
-                   hipStream_t st);
+                   hipStream_t st, int64_t nb_dag);
 int dag_list_key(const gps_ctx* ctx, int64_t nb);
 bool dag_block(const gps_ctx* ctx, int64_t nb);
 void dag_blocks(const gps_ctx* ctx, int64_t nb, std::vector<int>& sizes, int64_t& cnt);

@@ -52,10 +52,13 @@ def _same(a, b):
         assert float(a[k]) == float(b[k]), (k, a[k], b[k])
 
 
-@pytest.mark.parametrize("n,m", [(3000, 200), (6000, 1000), (9000, 2000), (5000, 2560)])
+@pytest.mark.parametrize("n,m", [(3000, 200), (6000, 1000), (9000, 2000), (5000, 2560),
+                                 (7000, 2900), (9000, 4000)])
 def test_fitc_dep_bitwise(gp, gpu_ctx, n, m):
-    """m_pad from 2 to 20 tiles (one persistent launch each): dependent row norms on and off
-    give the same bits; the oracle agrees as in the other FITC tests."""
+    """m_pad from 2 to 20 tiles (one persistent launch each: the whole q pass behind Lm's) and
+    23 / 32 tiles (a recursive factorisation, C5's shape: the q pre-pass over the top L11⁻¹
+    columns behind that block's launch, odd and even splits): dependent row norms on and
+    off give the same bits; the oracle agrees as in the other FITC tests."""
     from gpscore import _lib
     X, y, Xt, yt, Z, th = _case(n, 700, m, 8, 31 + m)
     runs = []
@@ -79,7 +82,17 @@ def test_fitc_dep_any_factorisation_width(gp, gpu_ctx, wgs):
     CUs can hold beside the row-norm launch: it must leave its tiles rather than wait for
     workgroups that are not resident).  Same bits as the sequential schedule every time."""
     from gpscore import _lib
-    X, y, Xt, yt, Z, th = _case(7000, 600, 2000, 8, 77)
+    _widths(gp, gpu_ctx, wgs, *_case(7000, 600, 2000, 8, 77))
+
+
+@pytest.mark.parametrize("wgs", [4, 1024])
+def test_fitc_dep_recursive_any_width(gp, gpu_ctx, wgs):
+    """The same for the recursive factorisation's pre-pass (m_pad 26 tiles, L11 of 13)."""
+    _widths(gp, gpu_ctx, wgs, *_case(6000, 600, 3300, 8, 78))
+
+
+def _widths(gp, gpu_ctx, wgs, X, y, Xt, yt, Z, th):
+    from gpscore import _lib
     try:
         gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_FITC_DEP, 0)
         base = _unit(gp, X, y, Xt, yt, Z, th)
