@@ -969,10 +969,13 @@ hipError_t launch_gemm(int alay, int blay, int epi, const GemmParams& pin, hipSt
   }
   const bool pairable = rowsq && q.tri == TRI_K_LE_J && tile == 128 && q.ksplit == 1;
   if (q.map_mode == 6 && !pairable) q.map_mode = 0;  // (an override of 6 leaves the rest automatic)
-  // pairs only with ≥ 4 rounds of the 512 workgroup slots: the uniform grid quantises — C4's
-  // test-side norms (79 × 8 pairs, 1.2 rounds) ran 1097 µs paired against 961 in map 5
-  // (profiles/r5k_rowsq_pairs_prof.txt)
-  const bool paired = pairable && (int64_t)q.tiles_m * ((q.tiles_n + 1) / 2) >= 2048;
+  // pairs for every pairable launch since round 6: round 5 kept the smaller grids (< 2048 pairs)
+  // in map 5 — C4's test-side norms ran 1097 µs paired against 961 then
+  // (profiles/r5k_rowsq_pairs_prof.txt) — but on the round-6 library the same 10 112-row shape
+  // runs 49.6 TF/s paired against 45.0 in map 5 (tools/gemm_bench rowsq_iso), and pairs on the
+  // small grids (the test-side norms, C5's pre-pass at 25 000 rows) measured C4 11.64 → 11.44 ms
+  // and C5r8 28.47 → 27.25 (profiles/r6q_rowsq_pairs_all_ab.txt)
+  const bool paired = pairable;
   if (q.map_mode == 0 && q.tri != TRI_NONE && q.tri != TRI_KR_J && !q.lower_out)
     q.map_mode = rowsq ? (paired ? 6 : 5) : 3;
   else if (q.map_mode == 4) q.map_mode = 0;  // 4: the previous automatic order (A/B runs)

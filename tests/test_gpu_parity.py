@@ -977,6 +977,41 @@ def test_gemm_slab_xcd_bitwise(gpu_ctx):
             assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("n,m", [(6000, 600), (9000, 1000), (3000, 130)])
+def test_rowsq_pairs_bitwise(gpu_ctx, n, m):
+    """The FITC row norms in paired column tiles — a workgroup runs column tiles T−1−q and q, the
+    automatic order of every row-norm launch over a triangular L⁻¹ since round 6 (map 6) —
+    against one tile per workgroup (map 5): odd T (m_pad 640: the middle tile alone), even T,
+    T = 2, through the q / r passes (EPI_ROWSQ, EPI_ROWSQ_DOT with g = Knm c), the test-side
+    norms, the LOO and predictive outputs and the θ / Z gradients: the same bits (only the
+    workgroup that runs a tile changes).  Reference: K20:222-234 (Q, G, big_Q), K20:76-83."""
+    import gpscore
+    from gpscore import _lib
+    rng = np.random.default_rng(n + m)
+    d = 5
+    X, Xt = rng.standard_normal((n, d)), rng.standard_normal((700, d))
+    y, yt = np.sin(X.sum(1)), np.sin(Xt.sum(1))
+    Z = X[rng.choice(n, m, replace=False)]
+    th = (0.0, np.log(1.4) * np.ones(d), np.log(0.03))
+    outs = []
+    try:
+        for mm in (0, 6, 5):
+            gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_GEMM_MAP, mm)
+            gf = gpscore.GP(ctx=gpu_ctx)
+            gf.set_data(X, y, kind="fitc", Z=Z)
+            gf.set_test(Xt, yt)
+            rf = gf.fit(theta=th)
+            mu, var = gf.predict()
+            _, g, objs = gf.value_and_grad(th, "loo_crps")
+            outs.append([rf.mu_loo, rf.var_loo, mu, var, g, objs["grad_Z"],
+                         np.array(list(rf.objectives.values()))])
+    finally:
+        gpu_ctx.call("gps_ctx_set_option", _lib.GPS_OPT_GEMM_MAP, 0)
+    for alt in outs[1:]:
+        for a, b in zip(alt, outs[0]):
+            assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("n,tiles", [(2560, 20), (4000, 40)])
 def test_persistent_queue_orders_bitwise(gpu_ctx, n, tiles):
     """GPS_OPT_DAG_ORDER: the queue order moves tasks between workgroups and in time, never the
