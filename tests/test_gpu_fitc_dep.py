@@ -53,7 +53,7 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("n,m", [(3000, 200), (6000, 1000), (9000, 2000), (5000, 2560),
-                                 (7000, 2900), (9000, 4000)])
+                                 (7000, 2900), (9000, 4000), (300, 250)])
 def test_fitc_dep_bitwise(gp, gpu_ctx, n, m):
     """m_pad from 2 to 20 tiles (one persistent launch each: the whole q pass behind Lm's) and
     23 / 32 tiles (a recursive factorisation, C5's shape: the q pre-pass over the top L11⁻¹

@@ -977,7 +977,7 @@ def test_gemm_slab_xcd_bitwise(gpu_ctx):
             assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("n,m", [(6000, 600), (9000, 1000), (3000, 130)])
+@pytest.mark.parametrize("n,m", [(6000, 600), (9000, 1000), (3000, 130), (200, 150)])
 def test_rowsq_pairs_bitwise(gpu_ctx, n, m):
     """The FITC row norms in paired column tiles — a workgroup runs column tiles T−1−q and q, the
     automatic order of every row-norm launch over a triangular L⁻¹ since round 6 (map 6) —
