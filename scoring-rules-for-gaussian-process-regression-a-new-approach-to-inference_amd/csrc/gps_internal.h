@@ -94,13 +94,14 @@ struct GemmParams {
   //     are resident, so the wait cannot starve them); otherwise it leaves the tile to
   //   dep_mode 2 (the completion launch, stream-ordered after the factorisation): block b is tile
   //     (b % tiles_m, tiles_n − 1 − b / tiles_m), skipped if the dependent launch took it.
-  const int* dep_sig; int* dep_q; int* dep_err; int dep_grid; int dep_mode;
+  int* dep_sig; int* dep_q; int* dep_err; int dep_grid; int dep_mode;
 };
 // The signal block of a persistent factorisation with a dependent row-norm launch (int words,
 // zeroed before the pair is launched; DagParams::sig, GemmParams::dep_sig / dep_q)
 constexpr int kSigStarted = 0;   // workgroups of the factorisation that have started
 constexpr int kSigRowCnt = 64;   // [64] per row tile of L⁻¹: FIN strips completed
-constexpr int kSigRdy = 128;     // [64] per row tile: 1 once the row of L⁻¹ is final
+constexpr int kSigRdy = 128;     // [64] per row tile: 1 once the row of L⁻¹ is final (2: and
+                                 // every band of that column taken by the dependent launch)
 constexpr int kSigQueue = 192;   // [8 XCDs][64 column tiles] queue heads of one dependent launch
 constexpr int kSigInts = kSigQueue + 8 * 64;
 

@@ -150,42 +150,60 @@ __device__ bool dep_take(const GemmParams& p, double* smem, int& ti, int& tj) {
     const int len = dep_band0(tm, x + 1) - dep_band0(tm, x);
     return ti - dep_band0(tm, x) >= min(p.dep_q[x * 64 + tj], len);
   }
+  // The take runs on wave 0's 64 lanes: one load per column state (lane j reads column j's)
+  // and one per band counter (lane l reads band me + l's) per round instead of a lane-0 walk that
+  // issued up to 9 dependent L2 round trips per exhausted column (round 5's dep_take; late in
+  // the launch a workgroup walked ~10 of them before finding work).  Column state in kSigRdy:
+  // 0 row not final, 1 final (the factorisation's store), 2 final and every band taken (set by
+  // the workgroup that found all eight counters at their band length; counters only grow).
   int* sh = reinterpret_cast<int*>(smem);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    const int lane = (int)threadIdx.x;
     unsigned int xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const int me = (int)(xcc & 7);
-    const int* rdy = p.dep_sig + kSigRdy;
+    int* st = p.dep_sig + kSigRdy;
+    const int xb = (me + lane) & 7;  // lane l < 8: band me + l (this XCD's own band first)
+    const int b0 = dep_band0(tm, xb), len = dep_band0(tm, xb + 1) - b0;
     int res = -1;
     unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int seen = -1;
     unsigned int polls = 0;
     for (;;) {
-      int nready = 0, first_wait = -1;
-      for (int j = T - 1; j >= 0 && res < 0; --j) {
-        if (!dep_ld(rdy + j)) { first_wait = j; continue; }
-        ++nready;
-        for (int o = 0; o < 8 && res < 0; ++o) {
-          const int x = (me + o) & 7, b0 = dep_band0(tm, x), len = dep_band0(tm, x + 1) - b0;
-          int* q = p.dep_q + x * 64 + j;
-          if (dep_ld(q) >= len) continue;
-          const int r = __hip_atomic_fetch_add(q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (r < len) res = (b0 + r) << 8 | j;
+      const int sv = lane < T ? dep_ld(st + lane) : 0;
+      const unsigned long long ready = __ballot(sv != 0);
+      unsigned long long cand = __ballot(sv == 1);
+      while (cand && res < 0) {
+        const int j = 63 - __builtin_clzll(cand);  // the heaviest final column not known taken
+        cand &= ~(1ull << j);
+        int* qj = p.dep_q + xb * 64 + j;
+        const int qv = lane < 8 ? dep_ld(qj) : 0;
+        unsigned long long open = __ballot(lane < 8 && qv < len);
+        while (open && res < 0) {
+          const int l = __builtin_ctzll(open);
+          open &= open - 1;
+          int r = 0;
+          if (lane == l) r = __hip_atomic_fetch_add(qj, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          r = __shfl(r, l);
+          const int lb0 = __shfl(b0, l), llen = __shfl(len, l);
+          if (r < llen) res = (lb0 + r) << 8 | j;
         }
+        if (res < 0 && lane == 0)
+          __hip_atomic_store(st + j, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (res >= 0 || nready == T) break;  // (all rows final and nothing left: cannot happen)
+      const int nready = __popcll(ready);
+      if (res >= 0 || nready == T) break;  // (all rows final and nothing left: the launch's tail)
       if (dep_ld(p.dep_err) != 0x7f7f7f7f) break;  // the factorisation failed: leave the tile
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
       if (dep_ld(p.dep_sig + kSigStarted) < p.dep_grid) {  // not all resident yet: ≤ 20 µs
         if (now - t0 > 2000) break;
       } else {  // wait for the next row (bounded: 2 s without a new row and 1e5 polls)
-        const int s = nready * 64 + first_wait;
-        if (s != seen) {
-          seen = s;
+        if (nready != seen) {
+          seen = nready;
           t0 = now;
           polls = 0;
         } else if (++polls > 100000u && now - t0 > 200000000ull) {
-          __hip_atomic_store(p.dep_err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(p.dep_err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -194,7 +212,7 @@ __device__ bool dep_take(const GemmParams& p, double* smem, int& ti, int& tj) {
     // agent-scope acquire: the rows' payload (stored write-through and drained before the
     // factorisation's arrivals) is visible to the operand loads after the barrier
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    sh[0] = res;
+    if (lane == 0) sh[0] = res;
   }
   __syncthreads();
   const int res = __builtin_amdgcn_readfirstlane(sh[0]);
