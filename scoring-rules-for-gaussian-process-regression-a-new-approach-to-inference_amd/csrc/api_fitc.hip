@@ -313,15 +313,20 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   // tiles — about what the CUs beside the launch finish while it runs; a larger one would run
   // on at the dependent launch's column-by-column rate, below the paired order's.  Measured
   // (DESIGN §6.49): C5's rows per rank at N = 8 / 4 (3136 / 6256 tiles) 28.88 → 28.76 / 49.01 →
-  // 48.81 ms, at N = 2 / 1 (12 512 / 25 008) 89.38 → 90.51 / 169.8 → 170.7.  Lb's r pre-pass stays
-  // after L11 (dependent: +0.6 ms at N = 8 — the test-side q* norms already hold those CUs)
+  // 48.81 ms, at N = 2 / 1 (12 512 / 25 008) 89.38 → 90.51 / 169.8 → 170.7
   const bool pdep = preq && ctx->fitc_dep && ctx->overlap && !ctx->prof &&
                     dag_block(ctx, tm / 2) && (np / GPS_TILE) * (tm / 2) <= 8192;
   int* sig_m = nullptr;
+  int* sig_b = nullptr;
+  // ... and the r pre-pass behind Lb's top L11 block the same way when it is at most 4096 tiles
+  // (once the dependent take was cheap, §6.46: C5r8, 3136 tiles, 27.18-27.28 → 27.05 ms; C5r4,
+  // 6256 tiles, 47.35-47.46 → 47.74-47.85; profiles/r6ae_fitc_rpre_dep_ab.txt)
+  const bool pdep_b = pdep && (np / GPS_TILE) * (tm / 2) <= 4096;
   if (dep || pdep) {  // (zeroed, stream-ordered before both launches of the pair)
-    HIPCHK(ensure(ctx, ctx->dsig, kSigInts * sizeof(int)));
+    HIPCHK(ensure(ctx, ctx->dsig, 2 * kSigInts * sizeof(int)));
     sig_m = static_cast<int*>(ctx->dsig.p);
-    HIPCHK(hipMemsetAsync(ctx->dsig.p, 0, kSigInts * sizeof(int), s));
+    sig_b = sig_m + kSigInts;
+    HIPCHK(hipMemsetAsync(ctx->dsig.p, 0, 2 * kSigInts * sizeof(int), s));
   }
   if (kside) {  // (dedicated events: the factorisation reuses its pool of sync events)
     for (hipEvent_t* e : {&ctx->kn_fork, &ctx->kn_join})
@@ -409,6 +414,7 @@ int fitc_fit_core(gps_ctx* ctx, const double* theta, int n_ell, double obj[GPS_N
   ctx->pre.kind = preq ? PRE_FITC_Q : PRE_NONE;
   ctx->pre.n1 = qn1;
   ctx->pre.L = ctx->Lb.d();
+  ctx->pre.sig = pdep_b ? sig_b : nullptr;
   // (the r pass behind Lb's factorisation as well — every column tile on aux[1], g = Knm c by a GEMV
   //  after c — measured no faster: C4 11.84 vs 11.80 ms, profiles/r6b_fitc_dep_ab_c4.txt; the CUs
   //  Lb's factorisation leaves already run the test-side q* norms)
