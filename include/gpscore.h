@@ -135,7 +135,8 @@ enum {
                              (device-side row signals), and a completion launch after it takes
                              the tiles left; with m_pad > 20 tiles (a recursive factorisation)
                              the same for the q pre-pass over the top-level L11⁻¹ columns when
-                             that block is one persistent launch and the pre-pass ≤ 8192 tiles;
+                             that block is one persistent launch and the pre-pass ≤ 8192 tiles,
+                             and for the r pre-pass behind Lb's L11 block at ≤ 4096 tiles;
                              0: the row norms after the factorisation.  Same tiles, same values
                              bitwise. */
 };
