@@ -370,17 +370,30 @@ int potrf_inv_rec(gps_ctx* ctx, double* A, int64_t lda, double* Linv, int64_t ld
   const bool pre_here = top && ctx->pre.kind == PRE_FITC_Q && ctx->pre.n1 == n1;
   const bool pre_dep = pre_here && ctx->pre.sig && ctx->overlap && dag_block(ctx, n1b);
   // (on aux[1]: aux[0] may still hold the test-side pre-pass, FIFO ahead of it)
+  // (an error return after the fork joins aux[1] first: no launch of this call may still run
+  //  beside the context's next one)
+  auto join_dep = [&]() {
+    if (!pre_dep) return;
+    hipEvent_t j = sync_event(ctx);
+    if (j && hipEventRecord(j, ctx->aux[1]) == hipSuccess) (void)hipStreamWaitEvent(s, j, 0);
+  };
   if (pre_dep) {
     hipEvent_t f = sync_event(ctx);
     if (!f) return fail(ctx, -2, "hipEventCreate failed");
     HIPCHK(hipEventRecord(f, s));
     HIPCHK(hipStreamWaitEvent(ctx->aux[1], f, 0));
-    if ((rc = fitc_rowsq_dep(ctx, Linv, ctx->pre.sig, n1, 1, ctx->aux[1], n1b))) return rc;
+    if ((rc = fitc_rowsq_dep(ctx, Linv, ctx->pre.sig, n1, 1, ctx->aux[1], n1b))) {
+      join_dep();
+      return rc;
+    }
     ctx->dag_sig = ctx->pre.sig;  // (consumed by rec(A11)'s persistent launch)
   }
   rc = potrf_inv_rec(ctx, A, lda, Linv, ldl, W, n1b, logdiag, info, base, nreal, Lout, ldlo);
   ctx->dag_sig = nullptr;
-  if (rc) return rc;
+  if (rc) {
+    join_dep();
+    return rc;
+  }
   {  // W = L21 = A21 · L11⁻ᵀ
     GemmParams p = gp0();
     p.A = A21; p.lda = lda; p.B = Linv; p.ldb = ldl; p.C = W; p.ldc = n1;
